@@ -1,0 +1,528 @@
+// dtmpc_device.hpp — CDNA4 device code for the batched DDP/IFT tube-MPC hot path.
+//
+// Mapping: ONE LANE PER TRAJECTORY.  A wave holds 64 independent trajectories;
+// every per-step tape (states, controls, gains) lives in HBM in SoA [step][field][B] order, so each
+// per-step load/store of a field is one fully coalesced 256 B (f32) line per wave.  The small
+// per-step blocks (4x4 Riccati matrices, 2x2 solves) stay in VGPRs, the obstacle parameters in
+// SGPRs.  The line search advances all L alphas in the same loop over k (L-wide ILP, one tape read
+// per step instead of L).
+//
+// Every function cites the reference (lmcggg/differentiable-tube-mpc) code it restates.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dtmpc.h"
+
+namespace dtmpc {
+
+// ---------------------------------------------------------------------------------------------
+// math helpers (precision-overloaded)
+__device__ __forceinline__ void m_sincos(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ __forceinline__ void m_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __forceinline__ float m_exp(float x) { return expf(x); }
+__device__ __forceinline__ double m_exp(double x) { return exp(x); }
+__device__ __forceinline__ float m_log(float x) { return logf(x); }
+__device__ __forceinline__ double m_log(double x) { return log(x); }
+__device__ __forceinline__ float m_atan2(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ double m_atan2(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ float m_abs(float x) { return fabsf(x); }
+__device__ __forceinline__ double m_abs(double x) { return fabs(x); }
+template <typename T>
+__device__ __forceinline__ bool finite(T x) {
+  return __builtin_isfinite(x);
+}
+// torch.clamp semantics: NaN propagates (core/control.py:61-64)
+template <typename T>
+__device__ __forceinline__ T clampv(T v, T lo, T hi) {
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+template <typename T>
+__device__ __forceinline__ T wrap_angle(T e) {  // run_nominal.py:32-34
+  T s, c;
+  m_sincos(e, &s, &c);
+  return m_atan2(s, c);
+}
+
+// ---------------------------------------------------------------------------------------------
+// typed problem description (built on the host from dtmpc_spec / dtmpc_cost / dtmpc_ilqr_cfg)
+template <typename T>
+struct DSpec {
+  int N, M, agg, barrier;
+  T dt, umin0, umin1, umax0, umax1, active_tol;
+  T neg_beta, neg_inv_beta;  // (-beta), -(1/beta) as the reference's python floats
+  T alpha, gamma, eps;
+  T cx[DTMPC_MAX_OBS], cy[DTMPC_MAX_OBS], r2[DTMPC_MAX_OBS];
+};
+
+template <typename T>
+struct DCost {
+  int kind, wrap;
+  T Q0, Q1, Q2, R0, R1, Qf0, Qf1, Qf2, qb, t0, t1, t2;
+};
+
+template <typename T>
+struct DIlqr {
+  int max_iter, na;
+  T tol, reg;
+  T alphas[DTMPC_MAX_ALPHAS];
+};
+
+// Per-thread strided view of one trajectory inside a SoA [rows][F][B] array.
+template <typename T>
+struct Col {
+  T* p;
+  int ld;  // B
+  __device__ __forceinline__ T& at(int k, int F, int f) const { return p[(k * F + f) * ld]; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// safety function h  (core/systems/dubins_obstacles.py)
+
+template <typename T>
+__device__ __forceinline__ T h_circle(const DSpec<T>& s, int i, T px, T py) {  // :16-30
+  T dx = px - s.cx[i];
+  T dy = py - s.cy[i];
+  return dx * dx + dy * dy - s.r2[i];
+}
+
+// h for W points at once (obstacle loop outer, points inner => W-wide ILP).
+//   smoothmin: h_multi_circle_obstacles :41-69 (stable LSE, two passes)
+//   min:       h_min_circle_obstacles :95-106
+//   single:    h_circle_obstacle :16-30;  none: 1 (run_nominal.py:256)
+template <typename T, int W>
+__device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* py, T* h) {
+  if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0) {
+    T zmax[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) zmax[w] = s.neg_beta * h_circle(s, 0, px[w], py[w]);
+    for (int i = 1; i < s.M; ++i) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        T z = s.neg_beta * h_circle(s, i, px[w], py[w]);
+        zmax[w] = z > zmax[w] ? z : zmax[w];
+      }
+    }
+    T se[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) se[w] = T(0);
+    for (int i = 0; i < s.M; ++i) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) se[w] += m_exp(s.neg_beta * h_circle(s, i, px[w], py[w]) - zmax[w]);
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) h[w] = s.neg_inv_beta * (zmax[w] + m_log(se[w]));
+  } else if (s.agg == DTMPC_OBS_MIN && s.M > 0) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) h[w] = h_circle(s, 0, px[w], py[w]);
+    for (int i = 1; i < s.M; ++i) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        T hi = h_circle(s, i, px[w], py[w]);
+        h[w] = hi < h[w] ? hi : h[w];
+      }
+    }
+  } else if (s.agg == DTMPC_OBS_SINGLE && s.M > 0) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) h[w] = h_circle(s, 0, px[w], py[w]);
+  } else {
+#pragma unroll
+    for (int w = 0; w < W; ++w) h[w] = T(1);
+  }
+}
+
+// h and dh/d(px,py) at one point (grad_h_multi_circle_obstacles :72-92,
+// grad_h_min_circle_obstacles :109-117, grad_h_circle_obstacle :33-38).  The softmax weights are
+// e_i * (1/sum e) instead of e_i / sum e (one reciprocal per point).
+template <typename T>
+__device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy) {
+  if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0) {
+    T zmax = s.neg_beta * h_circle(s, 0, px, py);
+    for (int i = 1; i < s.M; ++i) {
+      T z = s.neg_beta * h_circle(s, i, px, py);
+      zmax = z > zmax ? z : zmax;
+    }
+    T se = T(0), sx = T(0), sy = T(0);
+    for (int i = 0; i < s.M; ++i) {
+      T e = m_exp(s.neg_beta * h_circle(s, i, px, py) - zmax);
+      se += e;
+      sx += e * (T(2) * (px - s.cx[i]));
+      sy += e * (T(2) * (py - s.cy[i]));
+    }
+    T inv = T(1) / se;
+    gx = sx * inv;
+    gy = sy * inv;
+    return s.neg_inv_beta * (zmax + m_log(se));
+  }
+  if (s.agg == DTMPC_OBS_MIN && s.M > 0) {
+    int am = 0;
+    T hm = h_circle(s, 0, px, py);
+    for (int i = 1; i < s.M; ++i) {
+      T hi = h_circle(s, i, px, py);
+      if (hi < hm) {
+        hm = hi;
+        am = i;
+      }
+    }
+    gx = T(2) * (px - s.cx[am]);
+    gy = T(2) * (py - s.cy[am]);
+    return hm;
+  }
+  if (s.agg == DTMPC_OBS_SINGLE && s.M > 0) {
+    gx = T(2) * (px - s.cx[0]);
+    gy = T(2) * (py - s.cy[0]);
+    return h_circle(s, 0, px, py);
+  }
+  gx = T(0);
+  gy = T(0);
+  return T(1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// barriers (core/barrier.py, core/systems/dubins_aug_jac.py)
+
+// relaxed_inverse_barrier_B_alpha core/barrier.py:36-59, alpha_eff = max(alpha, eps)
+template <typename T>
+__device__ __forceinline__ T barrier_relaxed(const DSpec<T>& s, T z) {
+  T a = s.alpha > s.eps ? s.alpha : s.eps;
+  if (z >= a) {
+    T zc = z < s.eps ? s.eps : z;
+    return T(1) / zc;
+  }
+  T diff = z - a;
+  T a2 = a * a;
+  return (T(1) / a - diff / a2) + (diff * diff) / (a2 * a);
+}
+
+// _dB_relaxed_inv_dz core/systems/dubins_aug_jac.py:31-40
+template <typename T>
+__device__ __forceinline__ T dbarrier_relaxed(const DSpec<T>& s, T z) {
+  T a = s.alpha > s.eps ? s.alpha : s.eps;
+  if (z >= a) {
+    T zc = z < s.eps ? s.eps : z;
+    return T(-1) / (zc * zc);
+  }
+  T diff = z - a;
+  T a2 = a * a;
+  return -(T(1) / a2) + (T(2) * diff) / (a2 * a);
+}
+
+// barrier inside the DBaS dynamics (core/barrier.py:99-106; log: barrier_B :62-72)
+template <typename T>
+__device__ __forceinline__ T barrier_dyn(const DSpec<T>& s, T z) {
+  if (s.barrier == DTMPC_BARRIER_LOG) {
+    T zc = z < s.eps ? s.eps : z;
+    return -m_log(zc);
+  }
+  return barrier_relaxed(s, z);
+}
+
+// ---------------------------------------------------------------------------------------------
+// dynamics: W DBaS-augmented Dubins steps at once.
+//   x' = dubins_step(x, u)            core/systems/dubins.py:26-45
+//   b' = B(h(x')) - gamma (B(h(x)) - b) core/barrier.py:75-108
+// Bc[w] carries B(h(x_k)) from the previous step (the reference recomputes h(x_k) inside
+// dbas_step; the value is the same function of the same state), and is updated to B(h(x_{k+1})).
+template <typename T, int W>
+__device__ __forceinline__ void fhat_vec(const DSpec<T>& s, T* x0, T* x1, T* x2, T* b,
+                                         const T* u0, const T* u1, T* Bc) {
+  T hn[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    T sn, c;
+    m_sincos(x2[w], &sn, &c);
+    T dv = s.dt * u0[w];
+    x0[w] = x0[w] + dv * c;
+    x1[w] = x1[w] + dv * sn;
+    x2[w] = x2[w] + s.dt * u1[w];
+  }
+  h_vec<T, W>(s, x0, x1, hn);
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    T Bn = barrier_dyn(s, hn[w]);
+    b[w] = Bn - s.gamma * (Bc[w] - b[w]);
+    Bc[w] = Bn;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ T barrier_of_state(const DSpec<T>& s, T px, T py) {
+  T h[1], x[1] = {px}, y[1] = {py};
+  h_vec<T, 1>(s, x, y, h);
+  return barrier_dyn(s, h[0]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// costs (core/tube_mpc.py:823-842, 875-894; core/cost_derivs.py:58-146; run_nominal.py:297-324)
+
+template <typename T>
+__device__ __forceinline__ T stage_cost(const DCost<T>& c, T x0, T x1, T x2, T b, T u0, T u1,
+                                        T r0, T r1, T r2, T ur0, T ur1) {
+  T d0, d1, d2, e0, e1;
+  if (c.kind == DTMPC_COST_TRACK) {
+    d0 = x0 - r0;
+    d1 = x1 - r1;
+    d2 = x2 - r2;
+    e0 = u0 - ur0;
+    e1 = u1 - ur1;
+  } else {
+    d0 = x0 - c.t0;
+    d1 = x1 - c.t1;
+    d2 = x2 - c.t2;
+    if (c.wrap) d2 = wrap_angle(d2);
+    e0 = u0;
+    e1 = u1;
+  }
+  T sq = c.Q0 * d0 * d0 + c.Q1 * d1 * d1 + c.Q2 * d2 * d2;
+  T sr = c.R0 * e0 * e0 + c.R1 * e1 * e1;
+  return sq + sr + c.qb * (b * b);
+}
+
+template <typename T>
+__device__ __forceinline__ T term_cost(const DCost<T>& c, T x0, T x1, T x2, T b, T r0, T r1, T r2) {
+  T d0, d1, d2;
+  if (c.kind == DTMPC_COST_TRACK) {
+    d0 = x0 - r0;
+    d1 = x1 - r1;
+    d2 = x2 - r2;
+  } else {
+    d0 = x0 - c.t0;
+    d1 = x1 - c.t1;
+    d2 = x2 - c.t2;
+    if (c.wrap) d2 = wrap_angle(d2);
+  }
+  T sq = c.Qf0 * d0 * d0 + c.Qf1 * d1 * d1 + c.Qf2 * d2 * d2;
+  return sq + c.qb * (b * b);
+}
+
+// state error used by l_x / phi_x (wrapped target of run_nominal.py:311-320)
+template <typename T>
+__device__ __forceinline__ void deriv_dx(const DCost<T>& c, T x0, T x1, T x2, T r0, T r1, T r2,
+                                         T& d0, T& d1, T& d2) {
+  if (c.kind == DTMPC_COST_TRACK) {
+    d0 = x0 - r0;
+    d1 = x1 - r1;
+    d2 = x2 - r2;
+    return;
+  }
+  T t2 = c.t2;
+  if (c.wrap) t2 = x2 - wrap_angle(x2 - c.t2);
+  d0 = x0 - c.t0;
+  d1 = x1 - c.t1;
+  d2 = x2 - t2;
+}
+
+// ---------------------------------------------------------------------------------------------
+// sparse augmented Jacobian (core/systems/dubins_aug_jac.py:61-139)
+//   A = [[1,0,a02,0],[0,1,a12,0],[0,0,1,0],[a30,a31,a32,g]],  Bm = [[b00,0],[b10,0],[0,dt],[b30,b31]]
+template <typename T>
+struct Jac {
+  T a02, a12, a30, a31, a32, g, b00, b10, b21, b30, b31;
+};
+
+// (xk, uk): state/control at step k; (gxk, gyk, dBk): grad h and B' at x_k;
+// (gxn, gyn, dBn): the same at x_{k+1} = f(x_k, u_k).
+template <typename T>
+__device__ __forceinline__ Jac<T> make_jac(const DSpec<T>& s, T sn, T c, T v, T gxk, T gyk, T dBk,
+                                           T gxn, T gyn, T dBn) {
+  Jac<T> J;
+  T dt = s.dt;
+  J.a02 = -dt * v * sn;
+  J.a12 = dt * v * c;
+  J.b00 = dt * c;
+  J.b10 = dt * sn;
+  J.b21 = dt;
+  T r0 = dBn * gxn, r1 = dBn * gyn, r2 = dBn * T(0);
+  T gd = s.gamma * dBk;
+  // row_x = (dB_next dh_next)^T A3 - gamma dB_curr dh_curr   (:128-130)
+  J.a30 = r0 - gd * gxk;
+  J.a31 = r1 - gd * gyk;
+  J.a32 = (r0 * J.a02 + r1 * J.a12 + r2) - gd * T(0);
+  J.g = s.gamma;
+  // row_u = (dB_next dh_next)^T B3   (:131)
+  J.b30 = r0 * J.b00 + r1 * J.b10;
+  J.b31 = r2 * dt;
+  return J;
+}
+
+// ---------------------------------------------------------------------------------------------
+// 2x2 solves.  torch.linalg.solve = LU with partial pivoting (LAPACK getrf/getrs).
+template <typename T>
+struct LU2 {
+  bool sw;
+  T a00, a01, l, inv00, inv11;
+};
+
+template <typename T>
+__device__ __forceinline__ LU2<T> lu2(T m00, T m01, T m10, T m11) {
+  LU2<T> f;
+  f.sw = m_abs(m10) > m_abs(m00);
+  T a00 = f.sw ? m10 : m00, a01 = f.sw ? m11 : m01;
+  T a10 = f.sw ? m00 : m10, a11 = f.sw ? m01 : m11;
+  f.inv00 = T(1) / a00;
+  f.l = a10 * f.inv00;
+  T u11 = a11 - f.l * a01;
+  f.inv11 = T(1) / u11;
+  f.a00 = a00;
+  f.a01 = a01;
+  return f;
+}
+
+template <typename T>
+__device__ __forceinline__ void lu2_solve(const LU2<T>& f, T r0, T r1, T& x0, T& x1) {
+  T p0 = f.sw ? r1 : r0, p1 = f.sw ? r0 : r1;
+  T y1 = p1 - f.l * p0;
+  x1 = y1 * f.inv11;
+  x0 = (p0 - f.a01 * x1) * f.inv00;
+}
+
+// _solve_reduced core/ddp.py:23-60 for one right-hand side, given the active set.
+template <typename T>
+__device__ __forceinline__ void solve_reduced(const LU2<T>& f, T m00, T m11, bool act0, bool act1,
+                                              T r0, T r1, T& x0, T& x1) {
+  if (!act0 && !act1) {
+    lu2_solve(f, r0, r1, x0, x1);
+  } else {
+    x0 = (!act0 && act1) ? r0 / m00 : T(0);
+    x1 = (act0 && !act1) ? r1 / m11 : T(0);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// iLQR backward step with the sparse Jacobian (core/ddp.py:213-254).
+// l_xx = diag(lxx0..3), l_uu = diag(luu0,1), l_ux = 0.  Vx/Vxx are updated in place.
+template <typename T>
+struct Riccati {
+  T Vx[4];
+  T Vxx[4][4];
+};
+
+template <typename T>
+__device__ __forceinline__ bool riccati_step(const Jac<T>& J, const T* lx, const T* lu,
+                                             const T* lxx, const T* luu, T reg, Riccati<T>& R,
+                                             T* K, T* kff) {
+  const T(&V)[4][4] = R.Vxx;
+  const T* vx = R.Vx;
+  // Q_x = l_x + A^T V_x ; Q_u = l_u + B^T V_x
+  T Qx0 = lx[0] + (vx[0] + J.a30 * vx[3]);
+  T Qx1 = lx[1] + (vx[1] + J.a31 * vx[3]);
+  T Qx2 = lx[2] + (J.a02 * vx[0] + J.a12 * vx[1] + vx[2] + J.a32 * vx[3]);
+  T Qx3 = lx[3] + J.g * vx[3];
+  T Qu0 = lu[0] + (J.b00 * vx[0] + J.b10 * vx[1] + J.b30 * vx[3]);
+  T Qu1 = lu[1] + (J.b21 * vx[2] + J.b31 * vx[3]);
+  // A^T V_xx
+  T P[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    P[0][j] = V[0][j] + J.a30 * V[3][j];
+    P[1][j] = V[1][j] + J.a31 * V[3][j];
+    P[2][j] = J.a02 * V[0][j] + J.a12 * V[1][j] + V[2][j] + J.a32 * V[3][j];
+    P[3][j] = J.g * V[3][j];
+  }
+  // Q_xx = l_xx + (A^T V_xx) A
+  T Qxx[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    Qxx[i][0] = P[i][0] + P[i][3] * J.a30;
+    Qxx[i][1] = P[i][1] + P[i][3] * J.a31;
+    Qxx[i][2] = P[i][0] * J.a02 + P[i][1] * J.a12 + P[i][2] + P[i][3] * J.a32;
+    Qxx[i][3] = P[i][3] * J.g;
+    Qxx[i][i] = lxx[i] + Qxx[i][i];
+  }
+  // B^T V_xx
+  T S[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    S[0][j] = J.b00 * V[0][j] + J.b10 * V[1][j] + J.b30 * V[3][j];
+    S[1][j] = J.b21 * V[2][j] + J.b31 * V[3][j];
+  }
+  // Q_ux = (B^T V_xx) A ; Q_uu = l_uu + (B^T V_xx) B
+  T Qux[2][4], Quu[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    Qux[a][0] = S[a][0] + S[a][3] * J.a30;
+    Qux[a][1] = S[a][1] + S[a][3] * J.a31;
+    Qux[a][2] = S[a][0] * J.a02 + S[a][1] * J.a12 + S[a][2] + S[a][3] * J.a32;
+    Qux[a][3] = S[a][3] * J.g;
+    Quu[a][0] = S[a][0] * J.b00 + S[a][1] * J.b10 + S[a][3] * J.b30;
+    Quu[a][1] = S[a][2] * J.b21 + S[a][3] * J.b31;
+  }
+  Quu[0][0] = luu[0] + Quu[0][0];
+  Quu[1][1] = luu[1] + Quu[1][1];
+  // gains with the regularised Q_uu (:239-249)
+  LU2<T> f = lu2(Quu[0][0] + reg, Quu[0][1], Quu[1][0], Quu[1][1] + reg);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    T x0, x1;
+    lu2_solve(f, Qux[0][j], Qux[1][j], x0, x1);
+    K[j] = -x0;
+    K[4 + j] = -x1;
+  }
+  {
+    T x0, x1;
+    lu2_solve(f, Qu0, Qu1, x0, x1);
+    kff[0] = -x0;
+    kff[1] = -x1;
+  }
+  bool ok = finite(kff[0]) && finite(kff[1]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ok = ok && finite(K[j]);
+  // V_x = Q_x + K^T Q_uu k + K^T Q_u + Q_xu k  ;  V_xx = Q_xx + K^T Q_uu K + K^T Q_ux + Q_xu K
+  // (unregularised Q_uu, :251-252)
+  T KQ[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    KQ[i][0] = K[i] * Quu[0][0] + K[4 + i] * Quu[1][0];
+    KQ[i][1] = K[i] * Quu[0][1] + K[4 + i] * Quu[1][1];
+  }
+  T Qx[4] = {Qx0, Qx1, Qx2, Qx3};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    T t1 = KQ[i][0] * kff[0] + KQ[i][1] * kff[1];
+    T t2 = K[i] * Qu0 + K[4 + i] * Qu1;
+    T t3 = Qux[0][i] * kff[0] + Qux[1][i] * kff[1];
+    R.Vx[i] = Qx[i] + t1 + t2 + t3;
+  }
+  // K^T Q_ux and Q_xu K are transposes of each other (same products, commutative).
+  T M2[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) M2[i][j] = K[i] * Qux[0][j] + K[4 + i] * Qux[1][j];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      T m1 = KQ[i][0] * K[j] + KQ[i][1] * K[4 + j];
+      R.Vxx[i][j] = Qxx[i][j] + m1 + M2[i][j] + M2[j][i];
+    }
+  return ok;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10 (shared with oracle/dtmpc_oracle.c) -> disturbance w ~ U[low, high)^3
+__device__ __forceinline__ void philox4x32_10(uint64_t seed, uint64_t gidx, uint64_t step,
+                                              uint32_t* out) {
+  uint32_t c0 = (uint32_t)gidx, c1 = (uint32_t)(gidx >> 32), c2 = (uint32_t)step,
+           c3 = (uint32_t)(step >> 32);
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0;
+  out[1] = c1;
+  out[2] = c2;
+  out[3] = c3;
+}
+
+}  // namespace dtmpc

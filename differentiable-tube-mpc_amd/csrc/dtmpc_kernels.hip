@@ -1,0 +1,747 @@
+// dtmpc_kernels.hip — HIP kernels (gfx950) + the C ABI of include/dtmpc.h.
+//
+// One lane = one trajectory; 256-lane workgroups; grid = ceil(B / 256).  All arrays are SoA
+// [step][field][B] (include/dtmpc.h), so lane i of a wave touches element i of every 256 B line.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/dtmpc.h"
+#include "dtmpc_solver.hpp"
+
+namespace dtmpc {
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------------------------------------
+// host-side conversion of the C structs into the typed device descriptors
+template <typename T>
+static DSpec<T> make_spec(const dtmpc_spec& p) {
+  DSpec<T> s;
+  std::memset(&s, 0, sizeof(s));
+  s.N = p.horizon;
+  s.M = p.n_obstacles;
+  s.agg = p.obs_aggregation;
+  s.barrier = p.barrier_type;
+  s.dt = T(p.dt);
+  s.umin0 = T(p.u_min[0]);
+  s.umin1 = T(p.u_min[1]);
+  s.umax0 = T(p.u_max[0]);
+  s.umax1 = T(p.u_max[1]);
+  s.active_tol = T(p.active_tol);
+  s.neg_beta = T(-p.obs_beta);
+  s.neg_inv_beta = T(-(1.0 / p.obs_beta));
+  s.alpha = T(p.dbas_alpha);
+  s.gamma = T(p.dbas_gamma);
+  s.eps = T(p.dbas_eps);
+  for (int i = 0; i < p.n_obstacles && i < DTMPC_MAX_OBS; ++i) {
+    s.cx[i] = T(p.obs_cx[i]);
+    s.cy[i] = T(p.obs_cy[i]);
+    s.r2[i] = T(p.obs_r[i] * p.obs_r[i]);
+  }
+  return s;
+}
+
+template <typename T>
+static DCost<T> make_cost(const dtmpc_cost& c) {
+  DCost<T> o;
+  o.kind = c.kind;
+  o.wrap = c.wrap_angle;
+  o.Q0 = T(c.Q[0]);
+  o.Q1 = T(c.Q[1]);
+  o.Q2 = T(c.Q[2]);
+  o.R0 = T(c.R[0]);
+  o.R1 = T(c.R[1]);
+  o.Qf0 = T(c.Qf[0]);
+  o.Qf1 = T(c.Qf[1]);
+  o.Qf2 = T(c.Qf[2]);
+  o.qb = T(c.qb);
+  o.t0 = T(c.target[0]);
+  o.t1 = T(c.target[1]);
+  o.t2 = T(c.target[2]);
+  return o;
+}
+
+template <typename T>
+static DIlqr<T> make_ilqr(const dtmpc_ilqr_cfg& c) {
+  DIlqr<T> o;
+  std::memset(&o, 0, sizeof(o));
+  o.max_iter = c.max_iter;
+  o.na = c.n_alphas;
+  o.tol = T(c.tol);
+  o.reg = T(c.reg);
+  for (int a = 0; a < DTMPC_MAX_ALPHAS; ++a) o.alphas[a] = T(c.alphas[a]);
+  return o;
+}
+
+template <typename T>
+__device__ __forceinline__ Col<T> col(void* p, int64_t i, int B) {
+  Col<T> c;
+  c.p = p ? reinterpret_cast<T*>(p) + i : nullptr;
+  c.ld = B;
+  return c;
+}
+template <typename T>
+__device__ __forceinline__ Col<T> col(const void* p, int64_t i, int B) {
+  return col<T>(const_cast<void*>(p), i, B);
+}
+
+// ---------------------------------------------------------------------------------------------
+// KAT-level kernels
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) rollout_kernel(DSpec<T> s, int B, const void* x0,
+                                                         const void* U, void* X) {
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= B) return;
+  Col<T> cx0 = col<T>(x0, i, B);
+  T xs[4] = {cx0.at(0, 4, 0), cx0.at(0, 4, 1), cx0.at(0, 4, 2), cx0.at(0, 4, 3)};
+  rollout_traj(s, xs, col<T>(X, i, B), col<T>(U, i, B));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) dbas_init_kernel(DSpec<T> s, int B, const T* x, T* b) {
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= B) return;
+  b[i] = barrier_of_state(s, x[i], x[(size_t)B + i]);
+}
+
+// dense A [N][16], Bm [N][8], lx [N+1][4], lu [N][2] (dubins_augmented_jacobian + cost derivs)
+template <typename T>
+__global__ void __launch_bounds__(kBlock) linearize_kernel(DSpec<T> s, DCost<T> c, int B,
+                                                           const void* Xp, const void* Up,
+                                                           const void* Xrp, const void* Urp,
+                                                           void* Ap, void* Bp, void* lxp, void* lup) {
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= B) return;
+  const int N = s.N;
+  Col<T> X = col<T>(Xp, i, B), U = col<T>(Up, i, B), Xr = col<T>(Xrp, i, B), Ur = col<T>(Urp, i, B);
+  Col<T> A = col<T>(Ap, i, B), Bm = col<T>(Bp, i, B), LX = col<T>(lxp, i, B), LU = col<T>(lup, i, B);
+  T lxx[4], luu[2], pxx[4];
+  cost_diag(c, lxx, luu, pxx);
+  T r0, r1, r2, d0, d1, d2;
+  for (int k = 0; k < N; ++k) {
+    T x0 = X.at(k, 4, 0), x1 = X.at(k, 4, 1), x2 = X.at(k, 4, 2), xb = X.at(k, 4, 3);
+    T u0 = U.at(k, 2, 0), u1 = U.at(k, 2, 1);
+    T sn, cs;
+    m_sincos(x2, &sn, &cs);
+    T gxk, gyk, gxn, gyn;
+    T hk = h_grad(s, x0, x1, gxk, gyk);
+    T dv = s.dt * u0;
+    T n0 = x0 + dv * cs, n1 = x1 + dv * sn;
+    T hn = h_grad(s, n0, n1, gxn, gyn);
+    Jac<T> J = make_jac(s, sn, cs, u0, gxk, gyk, dbarrier_relaxed(s, hk), gxn, gyn,
+                        dbarrier_relaxed(s, hn));
+    T Ad[16] = {T(1), T(0), J.a02, T(0), T(0), T(1), J.a12, T(0),
+                T(0), T(0), T(1),  T(0), J.a30, J.a31, J.a32, J.g};
+    T Bd[8] = {J.b00, T(0), J.b10, T(0), T(0), J.b21, J.b30, J.b31};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) A.at(k, 16, j) = Ad[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Bm.at(k, 8, j) = Bd[j];
+    load_ref(c, Xr, 3, k, r0, r1, r2);
+    deriv_dx(c, x0, x1, x2, r0, r1, r2, d0, d1, d2);
+    LX.at(k, 4, 0) = lxx[0] * d0;
+    LX.at(k, 4, 1) = lxx[1] * d1;
+    LX.at(k, 4, 2) = lxx[2] * d2;
+    LX.at(k, 4, 3) = lxx[3] * xb;
+    T q0, q1;
+    load_uref(c, Ur, k, q0, q1);
+    if (c.kind == DTMPC_COST_TRACK) {
+      LU.at(k, 2, 0) = luu[0] * (u0 - q0);
+      LU.at(k, 2, 1) = luu[1] * (u1 - q1);
+    } else {
+      LU.at(k, 2, 0) = luu[0] * u0;
+      LU.at(k, 2, 1) = luu[1] * u1;
+    }
+  }
+  load_ref(c, Xr, 3, N, r0, r1, r2);
+  deriv_dx(c, X.at(N, 4, 0), X.at(N, 4, 1), X.at(N, 4, 2), r0, r1, r2, d0, d1, d2);
+  LX.at(N, 4, 0) = pxx[0] * d0;
+  LX.at(N, 4, 1) = pxx[1] * d1;
+  LX.at(N, 4, 2) = pxx[2] * d2;
+  LX.at(N, 4, 3) = pxx[3] * X.at(N, 4, 3);
+}
+
+// ---------------------------------------------------------------------------------------------
+// solver kernels
+
+template <typename T, int NA>
+__global__ void __launch_bounds__(kBlock) ilqr_kernel(DSpec<T> s, DCost<T> c, DIlqr<T> cfg, int B,
+                                                      const void* x0p, const void* Xrp,
+                                                      const void* Urp, void* Xp, void* Up,
+                                                      void* Kp, void* kfp, int* iters, int* status) {
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= B) return;
+  Col<T> cx0 = col<T>(x0p, i, B);
+  T x0[4] = {cx0.at(0, 4, 0), cx0.at(0, 4, 1), cx0.at(0, 4, 2), cx0.at(0, 4, 3)};
+  int it = 0;
+  int st = ilqr_traj<T, NA>(s, c, cfg, x0, col<T>(Xp, i, B), col<T>(Up, i, B), col<T>(Kp, i, B),
+                            col<T>(kfp, i, B), col<T>(Xrp, i, B), 3, col<T>(Urp, i, B), it);
+  if (iters) iters[i] = it;
+  if (status) status[i] |= st;
+}
+
+template <typename T, bool LAMBDA>
+__global__ void __launch_bounds__(kBlock) sens_kernel(DSpec<T> s, DCost<T> c, int B, const void* Xp,
+                                                      const void* Up, const void* Xrp,
+                                                      const void* Urp, const void* Xbp, void* dXp,
+                                                      void* dUp, void* dLp, void* work,
+                                                      int* status) {
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= B) return;
+  const int N = s.N;
+  T* w = reinterpret_cast<T*>(work);
+  const size_t nb = (size_t)B;
+  void* Kp = w;
+  void* kfp = w + (size_t)N * 8 * nb;
+  void* ABp = w + (size_t)N * 10 * nb;
+  void* VVp = w + (size_t)N * 20 * nb;
+  int st = sens_traj<T, LAMBDA, true, false>(
+      s, c, col<T>(Xp, i, B), col<T>(Up, i, B), col<T>(Xrp, i, B), 3, col<T>(Urp, i, B),
+      col<T>(Xbp, i, B), 3, col<T>(Kp, i, B), col<T>(kfp, i, B), col<T>(ABp, i, B),
+      col<T>(VVp, i, B), col<T>(dXp, i, B), col<T>(dUp, i, B), col<T>(dLp, i, B), nullptr);
+  if (status) status[i] |= st;
+}
+
+// upper loss + DOC gradient per trajectory (core/tube_mpc.py:915-919, 963-976); out [7][B]
+template <typename T>
+__global__ void __launch_bounds__(kBlock) docgrad_kernel(int N, int B, const void* Xap,
+                                                         const void* Uap, const void* Xnp,
+                                                         const void* Unp, const void* dXp,
+                                                         const void* dUp, void* outp) {
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= B) return;
+  Col<T> Xa = col<T>(Xap, i, B), Ua = col<T>(Uap, i, B), Xn = col<T>(Xnp, i, B),
+         Un = col<T>(Unp, i, B), dX = col<T>(dXp, i, B), dU = col<T>(dUp, i, B),
+         o = col<T>(outp, i, B);
+  T L1 = 0, L2 = 0, g0 = 0, g1 = 0, g2 = 0, r0 = 0, r1 = 0, gb = 0;
+  for (int k = 0; k <= N; ++k) {
+    T e0 = Xa.at(k, 4, 0) - Xn.at(k, 4, 0), e1 = Xa.at(k, 4, 1) - Xn.at(k, 4, 1),
+      e2 = Xa.at(k, 4, 2) - Xn.at(k, 4, 2), bb = Xa.at(k, 4, 3);
+    L1 += e0 * e0 + e1 * e1 + e2 * e2;
+    L2 += bb * bb;
+    g0 += T(2) * e0 * dX.at(k, 4, 0);
+    g1 += T(2) * e1 * dX.at(k, 4, 1);
+    g2 += T(2) * e2 * dX.at(k, 4, 2);
+    gb += T(2) * bb * dX.at(k, 4, 3);
+    if (k < N) {
+      r0 += T(2) * (Ua.at(k, 2, 0) - Un.at(k, 2, 0)) * dU.at(k, 2, 0);
+      r1 += T(2) * (Ua.at(k, 2, 1) - Un.at(k, 2, 1)) * dU.at(k, 2, 1);
+    }
+  }
+  o.at(0, 1, 0) = L1 + L2;
+  o.at(1, 1, 0) = g0;
+  o.at(2, 1, 0) = g1;
+  o.at(3, 1, 0) = g2;
+  o.at(4, 1, 0) = r0;
+  o.at(5, 1, 0) = r1;
+  o.at(6, 1, 0) = gb;
+}
+
+// ---------------------------------------------------------------------------------------------
+// fused closed-loop step (core/tube_mpc.py:803-1023 loop body)
+
+template <typename T>
+struct TubeArgs {
+  int B;
+  int64_t goff, step;
+  T* x;
+  T* b;
+  T* xbar;
+  T* bbar;
+  T* Xnom;
+  T* Unom;
+  T* Xaux;
+  T* Uaux;
+  T* work;
+  const T* theta;
+  T* partials;
+  T* log;
+  int* status;
+  int* iters;
+  const T* w;
+  int disturbance, write_log;
+  uint64_t seed;
+  T wlo[3], whi[3];
+};
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+template <typename T, int NA>
+__global__ void __launch_bounds__(kBlock) tube_step_kernel(DSpec<T> s, DCost<T> cn,
+                                                           DIlqr<T> cfn, DIlqr<T> cfa,
+                                                           TubeArgs<T> a) {
+  __shared__ T red[kBlock / 64][8];
+  const int B = a.B;
+  const int N = s.N;
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  T acc[7] = {T(0), T(0), T(0), T(0), T(0), T(0), T(0)};
+  if (i < B) {
+    const size_t nb = (size_t)B;
+    Col<T> Xn = col<T>(a.Xnom, i, B), Un = col<T>(a.Unom, i, B), Xa = col<T>(a.Xaux, i, B),
+           Ua = col<T>(a.Uaux, i, B);
+    Col<T> K = col<T>(a.work, i, B), kf = col<T>(a.work + (size_t)N * 8 * nb, i, B),
+           AB = col<T>(a.work + (size_t)N * 10 * nb, i, B);
+    T x0 = a.x[i], x1 = a.x[nb + i], x2 = a.x[2 * nb + i], xb = a.b[i];
+    T y0 = a.xbar[i], y1 = a.xbar[nb + i], y2 = a.xbar[2 * nb + i], yb = a.bbar[i];
+    int st = 0, itn = 0, ita = 0;
+    // nominal MPC solve (fixed weights) :813-857
+    T xn0[4] = {y0, y1, y2, yb};
+    Col<T> none = col<T>((void*)nullptr, i, B);
+    st |= ilqr_traj<T, NA>(s, cn, cfn, xn0, Xn, Un, K, kf, none, 0, none, itn);
+    // ancillary MPC tracking the nominal plan :863-909 (terminal weight Qa, :885, :891)
+    DCost<T> ca;
+    ca.kind = DTMPC_COST_TRACK;
+    ca.wrap = 0;
+    ca.Q0 = ca.Qf0 = a.theta[0];
+    ca.Q1 = ca.Qf1 = a.theta[1];
+    ca.Q2 = ca.Qf2 = a.theta[2];
+    ca.R0 = a.theta[3];
+    ca.R1 = a.theta[4];
+    ca.qb = a.theta[5];
+    ca.t0 = ca.t1 = ca.t2 = T(0);
+    T xa0[4] = {x0, x1, x2, xb};
+    st |= ilqr_traj<T, NA>(s, ca, cfa, xa0, Xa, Ua, K, kf, Xn, 4, Un, ita);
+    // upper loss, DOC sensitivity and analytic gradient :915-976
+    st |= sens_traj<T, false, false, true>(s, ca, Xa, Ua, Xn, 4, Un, Xn, 4, K, kf, AB, none, none,
+                                           none, none, acc);
+    // plant step with disturbance, nominal propagation :990-1001
+    T u0 = Ua.at(0, 2, 0), u1 = Ua.at(0, 2, 1);
+    T v0 = Un.at(0, 2, 0), v1 = Un.at(0, 2, 1);
+    T w[3];
+    if (a.disturbance == 0) {
+      w[0] = a.w[i];
+      w[1] = a.w[nb + i];
+      w[2] = a.w[2 * nb + i];
+    } else {
+      uint32_t r[4];
+      philox4x32_10(a.seed, (uint64_t)(a.goff + i), (uint64_t)a.step, r);
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        T u = T(r[f] >> 8) * T(1.0 / 16777216.0);
+        w[f] = a.wlo[f] + (a.whi[f] - a.wlo[f]) * u;
+      }
+    }
+    if (a.write_log) {
+      T* lg = a.log;
+      lg[i] = x0;
+      lg[nb + i] = x1;
+      lg[2 * nb + i] = x2;
+      lg[3 * nb + i] = u0;
+      lg[4 * nb + i] = u1;
+      lg[5 * nb + i] = y0;
+      lg[6 * nb + i] = y1;
+      lg[7 * nb + i] = y2;
+      lg[8 * nb + i] = v0;
+      lg[9 * nb + i] = v1;
+      lg[10 * nb + i] = xb;
+      lg[11 * nb + i] = acc[0];
+    }
+    {
+      T p0[1] = {x0}, p1[1] = {x1}, p2[1] = {x2}, pb[1] = {xb}, q0[1] = {u0}, q1[1] = {u1};
+      T Bc[1] = {barrier_of_state(s, x0, x1)};
+      fhat_vec<T, 1>(s, p0, p1, p2, pb, q0, q1, Bc);
+      a.x[i] = p0[0] + w[0];
+      a.x[nb + i] = p1[0] + w[1];
+      a.x[2 * nb + i] = p2[0] + w[2];
+      a.b[i] = pb[0];
+    }
+    {
+      T p0[1] = {y0}, p1[1] = {y1}, p2[1] = {y2}, pb[1] = {yb}, q0[1] = {v0}, q1[1] = {v1};
+      T Bc[1] = {barrier_of_state(s, y0, y1)};
+      fhat_vec<T, 1>(s, p0, p1, p2, pb, q0, q1, Bc);
+      a.xbar[i] = p0[0];
+      a.xbar[nb + i] = p1[0];
+      a.xbar[2 * nb + i] = p2[0];
+      a.bbar[i] = pb[0];
+    }
+    // warm-start shift V <- [V[1:], V[-1]]  :1015-1020
+    for (int k = 0; k + 1 < N; ++k) {
+      Un.at(k, 2, 0) = Un.at(k + 1, 2, 0);
+      Un.at(k, 2, 1) = Un.at(k + 1, 2, 1);
+      Ua.at(k, 2, 0) = Ua.at(k + 1, 2, 0);
+      Ua.at(k, 2, 1) = Ua.at(k + 1, 2, 1);
+    }
+    if (st) {
+#pragma unroll
+      for (int j = 0; j < 7; ++j) acc[j] = T(0);
+    }
+    a.status[i] |= st;
+    if (a.iters) {
+      a.iters[i] = itn;
+      a.iters[nb + i] = ita;
+    }
+  }
+  // fixed-order workgroup sum of [L, gQ, gR, gqb]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    T v = wave_sum(acc[j]);
+    if (lane == 0) red[wv][j] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    T v = T(0);
+    if (threadIdx.x < 7) {
+#pragma unroll
+      for (int q = 0; q < kBlock / 64; ++q) v += red[q][threadIdx.x];
+    }
+    a.partials[(size_t)blockIdx.x * 8 + threadIdx.x] = v;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) partials_reduce_kernel(int64_t n, const T* p, T* sums) {
+  __shared__ T red[kBlock][8];
+  T v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t r = threadIdx.x; r < n; r += kBlock)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += p[r * 8 + j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = v[j];
+  __syncthreads();
+  for (int h = kBlock / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[threadIdx.x][j] += red[threadIdx.x + h][j];
+    __syncthreads();
+  }
+  if (threadIdx.x < 8) sums[threadIdx.x] = red[0][threadIdx.x];
+}
+
+// momentum + projected update (core/tube_mpc.py:978-984)
+template <typename T>
+__global__ void theta_update_kernel(T mom, T eta, T qmin, T rmin, T qbmin, T qbmax, T inv_batch,
+                                    const T* sums, T* theta, T* vel) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int j = 0; j < 6; ++j) {
+    T g = sums[1 + j] * inv_batch;
+    vel[j] = mom * vel[j] + g;
+    T t = theta[j] - eta * vel[j];
+    if (j < 3)
+      theta[j] = t < qmin ? qmin : t;
+    else if (j < 5)
+      theta[j] = t < rmin ? rmin : t;
+    else
+      theta[j] = clampv(t, qbmin, qbmax);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host dispatch
+
+static thread_local char g_err[512] = "";
+
+static int set_err(int code, const char* msg) {
+  std::snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+
+static int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    std::snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return DTMPC_ERR_HIP;
+  }
+  return DTMPC_OK;
+}
+
+static int check_spec(const dtmpc_spec* s, int64_t B) {
+  if (!s) return set_err(DTMPC_ERR_BAD_ARG, "spec is NULL");
+  if (s->horizon < 1 || s->horizon > DTMPC_MAX_HORIZON) return set_err(DTMPC_ERR_BAD_ARG, "horizon out of range");
+  if (s->n_obstacles < 0 || s->n_obstacles > DTMPC_MAX_OBS) return set_err(DTMPC_ERR_BAD_ARG, "n_obstacles out of range");
+  if (s->obs_aggregation < 0 || s->obs_aggregation > DTMPC_OBS_NONE) return set_err(DTMPC_ERR_BAD_ARG, "bad obs_aggregation");
+  if (s->barrier_type != DTMPC_BARRIER_INVERSE && s->barrier_type != DTMPC_BARRIER_LOG) return set_err(DTMPC_ERR_BAD_ARG, "bad barrier_type");
+  if (s->dbas_alpha < 0) return set_err(DTMPC_ERR_BAD_ARG, "alpha must be >= 0");
+  if (!(s->dbas_gamma >= -1.0 && s->dbas_gamma <= 1.0)) return set_err(DTMPC_ERR_BAD_ARG, "gamma must be in [-1, 1]");
+  if (s->obs_aggregation == DTMPC_OBS_SMOOTHMIN && !(s->obs_beta > 0)) return set_err(DTMPC_ERR_BAD_ARG, "obs_beta must be > 0");
+  if (B < 1) return set_err(DTMPC_ERR_BAD_ARG, "batch must be >= 1");
+  // 32-bit in-kernel offsets: (rows * fields) * B must fit
+  if ((int64_t)(s->horizon + 1) * 20 * B >= (int64_t)1 << 31) return set_err(DTMPC_ERR_BAD_ARG, "batch too large for 32-bit tape offsets");
+  return DTMPC_OK;
+}
+
+static int check_ilqr(const dtmpc_ilqr_cfg* c) {
+  if (!c) return set_err(DTMPC_ERR_BAD_ARG, "ilqr cfg is NULL");
+  if (c->n_alphas < 1 || c->n_alphas > DTMPC_MAX_ALPHAS) return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
+  if (c->max_iter < 0) return set_err(DTMPC_ERR_BAD_ARG, "max_iter must be >= 0");
+  return DTMPC_OK;
+}
+
+static int check_cost(const dtmpc_cost* c, const void* Xref, const void* Uref) {
+  if (!c) return set_err(DTMPC_ERR_BAD_ARG, "cost is NULL");
+  if (c->kind != DTMPC_COST_TARGET && c->kind != DTMPC_COST_TRACK) return set_err(DTMPC_ERR_BAD_ARG, "bad cost kind");
+  if (c->kind == DTMPC_COST_TRACK && (!Xref || !Uref)) return set_err(DTMPC_ERR_BAD_ARG, "tracking cost needs Xref and Uref");
+  return DTMPC_OK;
+}
+
+static inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + kBlock - 1) / kBlock)); }
+
+template <typename T, int NA>
+static void launch_ilqr_na(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, int B,
+                           const void* x0, const void* Xref, const void* Uref, void* X, void* U,
+                           void* K, void* kff, int* iters, int* status, hipStream_t st) {
+  hipLaunchKernelGGL((ilqr_kernel<T, NA>), grid_for(B), dim3(kBlock), 0, st, s, c, cfg, B, x0, Xref,
+                     Uref, X, U, K, kff, iters, status);
+}
+
+template <typename T>
+static int launch_ilqr(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf,
+                       int64_t B, const void* x0, const void* Xref, const void* Uref, void* X,
+                       void* U, void* K, void* kff, int* iters, int* status, hipStream_t st) {
+  DSpec<T> s = make_spec<T>(*sp);
+  DCost<T> c = make_cost<T>(*cp);
+  DIlqr<T> cfg = make_ilqr<T>(*cf);
+  switch (cf->n_alphas) {
+#define CASE(n) \
+  case n: launch_ilqr_na<T, n>(s, c, cfg, (int)B, x0, Xref, Uref, X, U, K, kff, iters, status, st); break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+    default: return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
+  }
+  return check_launch("ilqr_kernel");
+}
+
+template <typename T>
+static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff,
+                       int64_t step, const dtmpc_tube_state* S, const void* w, hipStream_t st) {
+  DSpec<T> s = make_spec<T>(*sp);
+  DCost<T> cn = make_cost<T>(cf->nominal);
+  DIlqr<T> cfn = make_ilqr<T>(cf->nom_ilqr), cfa = make_ilqr<T>(cf->aux_ilqr);
+  TubeArgs<T> a;
+  std::memset(&a, 0, sizeof(a));
+  a.B = (int)B;
+  a.goff = goff;
+  a.step = step;
+  a.x = (T*)S->x;
+  a.b = (T*)S->b;
+  a.xbar = (T*)S->xbar;
+  a.bbar = (T*)S->bbar;
+  a.Xnom = (T*)S->Xnom;
+  a.Unom = (T*)S->Unom;
+  a.Xaux = (T*)S->Xaux;
+  a.Uaux = (T*)S->Uaux;
+  a.work = (T*)S->work;
+  a.theta = (const T*)S->theta;
+  a.partials = (T*)S->partials;
+  a.log = (T*)S->log;
+  a.status = S->status;
+  a.iters = S->iters;
+  a.w = (const T*)w;
+  a.disturbance = cf->disturbance;
+  a.write_log = (cf->write_log && S->log) ? 1 : 0;
+  a.seed = cf->seed;
+  for (int f = 0; f < 3; ++f) {
+    a.wlo[f] = T(cf->w_low[f]);
+    a.whi[f] = T(cf->w_high[f]);
+  }
+  // the fused kernel runs both solves with one line-search width
+  int na = cf->nom_ilqr.n_alphas;
+  switch (na) {
+#define CASE(n)                                                                                     \
+  case n:                                                                                           \
+    hipLaunchKernelGGL((tube_step_kernel<T, n>), grid_for(B), dim3(kBlock), 0, st, s, cn, cfn, cfa, a); \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+    default: return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
+  }
+  return check_launch("tube_step_kernel");
+}
+
+}  // namespace dtmpc
+
+using namespace dtmpc;
+
+extern "C" {
+
+int dtmpc_abi_version(void) { return DTMPC_ABI_VERSION; }
+
+const char* dtmpc_last_error(void) { return g_err; }
+
+int dtmpc_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int dtmpc_dbas_rollout(int dtype, const dtmpc_spec* spec, int64_t B, const void* x0, const void* U,
+                       void* X, void* stream) {
+  int e = check_spec(spec, B);
+  if (e) return e;
+  if (!x0 || !U || !X) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DTMPC_F32)
+    hipLaunchKernelGGL(rollout_kernel<float>, grid_for(B), dim3(kBlock), 0, st, make_spec<float>(*spec), (int)B, x0, U, X);
+  else if (dtype == DTMPC_F64)
+    hipLaunchKernelGGL(rollout_kernel<double>, grid_for(B), dim3(kBlock), 0, st, make_spec<double>(*spec), (int)B, x0, U, X);
+  else
+    return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+  return check_launch("rollout_kernel");
+}
+
+int dtmpc_dbas_init(int dtype, const dtmpc_spec* spec, int64_t B, const void* x, void* b,
+                    void* stream) {
+  int e = check_spec(spec, B);
+  if (e) return e;
+  if (!x || !b) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DTMPC_F32)
+    hipLaunchKernelGGL(dbas_init_kernel<float>, grid_for(B), dim3(kBlock), 0, st, make_spec<float>(*spec), (int)B, (const float*)x, (float*)b);
+  else if (dtype == DTMPC_F64)
+    hipLaunchKernelGGL(dbas_init_kernel<double>, grid_for(B), dim3(kBlock), 0, st, make_spec<double>(*spec), (int)B, (const double*)x, (double*)b);
+  else
+    return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+  return check_launch("dbas_init_kernel");
+}
+
+int dtmpc_linearize(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, int64_t B,
+                    const void* X, const void* U, const void* Xref, const void* Uref, void* A,
+                    void* Bm, void* lx, void* lu, void* stream) {
+  int e = check_spec(spec, B);
+  if (e) return e;
+  if ((e = check_cost(cost, Xref, Uref))) return e;
+  if (!X || !U || !A || !Bm || !lx || !lu) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DTMPC_F32)
+    hipLaunchKernelGGL(linearize_kernel<float>, grid_for(B), dim3(kBlock), 0, st, make_spec<float>(*spec), make_cost<float>(*cost), (int)B, X, U, Xref, Uref, A, Bm, lx, lu);
+  else if (dtype == DTMPC_F64)
+    hipLaunchKernelGGL(linearize_kernel<double>, grid_for(B), dim3(kBlock), 0, st, make_spec<double>(*spec), make_cost<double>(*cost), (int)B, X, U, Xref, Uref, A, Bm, lx, lu);
+  else
+    return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+  return check_launch("linearize_kernel");
+}
+
+int dtmpc_ilqr_solve(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
+                     const dtmpc_ilqr_cfg* cfg, int64_t B, const void* x0, const void* Xref,
+                     const void* Uref, void* X, void* U, void* K, void* kff, int32_t* iters,
+                     int32_t* status, void* stream) {
+  int e = check_spec(spec, B);
+  if (e) return e;
+  if ((e = check_cost(cost, Xref, Uref))) return e;
+  if ((e = check_ilqr(cfg))) return e;
+  if (!x0 || !X || !U || !K || !kff || !status) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DTMPC_F32) return launch_ilqr<float>(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, st);
+  if (dtype == DTMPC_F64) return launch_ilqr<double>(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, st);
+  return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+}
+
+size_t dtmpc_sensitivity_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t want_lambda) {
+  size_t el = dtype == DTMPC_F64 ? 8 : 4;
+  size_t per = (size_t)horizon * 20 + (want_lambda ? (size_t)(horizon + 1) * 20 : 0);
+  return el * per * (size_t)B;
+}
+
+int dtmpc_ddp_sensitivity(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, int64_t B,
+                          const void* X, const void* U, const void* Xref, const void* Uref,
+                          const void* Xbar, void* dX, void* dU, void* dlam, void* work,
+                          int32_t* status, void* stream) {
+  int e = check_spec(spec, B);
+  if (e) return e;
+  if ((e = check_cost(cost, Xref, Uref))) return e;
+  if (!X || !U || !Xbar || !dX || !dU || !work || !status) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DTMPC_F32) {
+    DSpec<float> s = make_spec<float>(*spec);
+    DCost<float> c = make_cost<float>(*cost);
+    if (dlam)
+      hipLaunchKernelGGL((sens_kernel<float, true>), grid_for(B), dim3(kBlock), 0, st, s, c, (int)B, X, U, Xref, Uref, Xbar, dX, dU, dlam, work, status);
+    else
+      hipLaunchKernelGGL((sens_kernel<float, false>), grid_for(B), dim3(kBlock), 0, st, s, c, (int)B, X, U, Xref, Uref, Xbar, dX, dU, dlam, work, status);
+  } else if (dtype == DTMPC_F64) {
+    DSpec<double> s = make_spec<double>(*spec);
+    DCost<double> c = make_cost<double>(*cost);
+    if (dlam)
+      hipLaunchKernelGGL((sens_kernel<double, true>), grid_for(B), dim3(kBlock), 0, st, s, c, (int)B, X, U, Xref, Uref, Xbar, dX, dU, dlam, work, status);
+    else
+      hipLaunchKernelGGL((sens_kernel<double, false>), grid_for(B), dim3(kBlock), 0, st, s, c, (int)B, X, U, Xref, Uref, Xbar, dX, dU, dlam, work, status);
+  } else {
+    return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+  }
+  return check_launch("sens_kernel");
+}
+
+int dtmpc_doc_grad(int dtype, int32_t horizon, int64_t B, const void* Xaux, const void* Uaux,
+                   const void* Xnom, const void* Unom, const void* dX, const void* dU, void* out,
+                   void* stream) {
+  if (horizon < 1 || horizon > DTMPC_MAX_HORIZON || B < 1) return set_err(DTMPC_ERR_BAD_ARG, "bad sizes");
+  if (!Xaux || !Uaux || !Xnom || !Unom || !dX || !dU || !out) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DTMPC_F32)
+    hipLaunchKernelGGL(docgrad_kernel<float>, grid_for(B), dim3(kBlock), 0, st, horizon, (int)B, Xaux, Uaux, Xnom, Unom, dX, dU, out);
+  else if (dtype == DTMPC_F64)
+    hipLaunchKernelGGL(docgrad_kernel<double>, grid_for(B), dim3(kBlock), 0, st, horizon, (int)B, Xaux, Uaux, Xnom, Unom, dX, dU, out);
+  else
+    return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+  return check_launch("docgrad_kernel");
+}
+
+size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
+  size_t el = dtype == DTMPC_F64 ? 8 : 4;
+  return el * (size_t)horizon * 20 * (size_t)B;
+}
+
+int64_t dtmpc_tube_partials_count(int64_t B) { return (B + kBlock - 1) / kBlock; }
+
+int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B,
+                    int64_t global_offset, int64_t step, const dtmpc_tube_state* state,
+                    const void* w, void* stream) {
+  int e = check_spec(spec, B);
+  if (e) return e;
+  if (!cfg || !state) return set_err(DTMPC_ERR_BAD_ARG, "NULL cfg/state");
+  if ((e = check_ilqr(&cfg->nom_ilqr)) || (e = check_ilqr(&cfg->aux_ilqr))) return e;
+  if (cfg->nom_ilqr.n_alphas != cfg->aux_ilqr.n_alphas)
+    return set_err(DTMPC_ERR_BAD_ARG, "nominal and ancillary line searches must have the same width");
+  for (int a = 0; a < cfg->nom_ilqr.n_alphas; ++a)
+    if (cfg->nom_ilqr.alphas[a] != cfg->aux_ilqr.alphas[a])
+      return set_err(DTMPC_ERR_BAD_ARG, "nominal and ancillary alphas must match");
+  if (cfg->nominal.kind != DTMPC_COST_TARGET) return set_err(DTMPC_ERR_BAD_ARG, "nominal cost must be DTMPC_COST_TARGET");
+  const dtmpc_tube_state* S = state;
+  if (!S->x || !S->b || !S->xbar || !S->bbar || !S->Xnom || !S->Unom || !S->Xaux || !S->Uaux ||
+      !S->work || !S->theta || !S->partials || !S->status)
+    return set_err(DTMPC_ERR_BAD_ARG, "NULL state array");
+  if (cfg->disturbance == 0 && !w) return set_err(DTMPC_ERR_BAD_ARG, "injected disturbance w is NULL");
+  if (cfg->disturbance != 0 && cfg->disturbance != 1) return set_err(DTMPC_ERR_BAD_ARG, "bad disturbance mode");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DTMPC_F32) return launch_tube<float>(spec, cfg, B, global_offset, step, S, w, st);
+  if (dtype == DTMPC_F64) return launch_tube<double>(spec, cfg, B, global_offset, step, S, w, st);
+  return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+}
+
+int dtmpc_partials_reduce(int dtype, int64_t n, const void* partials, void* sums, void* stream) {
+  if (n < 1 || !partials || !sums) return set_err(DTMPC_ERR_BAD_ARG, "bad partials");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DTMPC_F32)
+    hipLaunchKernelGGL(partials_reduce_kernel<float>, dim3(1), dim3(kBlock), 0, st, n, (const float*)partials, (float*)sums);
+  else if (dtype == DTMPC_F64)
+    hipLaunchKernelGGL(partials_reduce_kernel<double>, dim3(1), dim3(kBlock), 0, st, n, (const double*)partials, (double*)sums);
+  else
+    return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+  return check_launch("partials_reduce_kernel");
+}
+
+int dtmpc_theta_update(int dtype, const dtmpc_adapt_cfg* c, double inv_batch, const void* sums,
+                       void* theta, void* vel, void* stream) {
+  if (!c || !sums || !theta || !vel) return set_err(DTMPC_ERR_BAD_ARG, "NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DTMPC_F32)
+    hipLaunchKernelGGL(theta_update_kernel<float>, dim3(1), dim3(64), 0, st, (float)c->momentum, (float)c->lr_eta, (float)c->q_min, (float)c->r_min, (float)c->qb_min, (float)c->qb_max, (float)inv_batch, (const float*)sums, (float*)theta, (float*)vel);
+  else if (dtype == DTMPC_F64)
+    hipLaunchKernelGGL(theta_update_kernel<double>, dim3(1), dim3(64), 0, st, c->momentum, c->lr_eta, c->q_min, c->r_min, c->qb_min, c->qb_max, inv_batch, (const double*)sums, (double*)theta, (double*)vel);
+  else
+    return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+  return check_launch("theta_update_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,498 @@
+// dtmpc_solver.hpp — per-trajectory solver bodies (one lane = one trajectory).
+//
+//   ilqr_traj      core/ddp.py:102-307  ilqr_solve (typed: Dubins + DBaS + obstacles + quad cost)
+//   sens_traj      core/ddp.py:317-427  ddp_sensitivity with the paper upper loss
+//                  (core/tube_mpc.py:924-957) and, fused, the DOC gradient (:963-976)
+#pragma once
+
+#include "dtmpc_device.hpp"
+
+namespace dtmpc {
+
+template <typename T>
+__device__ __forceinline__ void cost_diag(const DCost<T>& c, T* lxx, T* luu, T* pxx) {
+  lxx[0] = T(2) * c.Q0;
+  lxx[1] = T(2) * c.Q1;
+  lxx[2] = T(2) * c.Q2;
+  lxx[3] = T(2) * c.qb;
+  luu[0] = T(2) * c.R0;
+  luu[1] = T(2) * c.R1;
+  pxx[0] = T(2) * c.Qf0;
+  pxx[1] = T(2) * c.Qf1;
+  pxx[2] = T(2) * c.Qf2;
+  pxx[3] = T(2) * c.qb;
+}
+
+template <typename T>
+__device__ __forceinline__ void load_ref(const DCost<T>& c, const Col<T>& Xr, int rf, int k, T& r0,
+                                         T& r1, T& r2) {
+  if (c.kind == DTMPC_COST_TRACK) {
+    r0 = Xr.at(k, rf, 0);
+    r1 = Xr.at(k, rf, 1);
+    r2 = Xr.at(k, rf, 2);
+  } else {
+    r0 = r1 = r2 = T(0);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void load_uref(const DCost<T>& c, const Col<T>& Ur, int k, T& q0, T& q1) {
+  if (c.kind == DTMPC_COST_TRACK) {
+    q0 = Ur.at(k, 2, 0);
+    q1 = Ur.at(k, 2, 1);
+  } else {
+    q0 = q1 = T(0);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// backward pass (core/ddp.py:172-254): linearise along (X, U) and run the Riccati recursion,
+// writing K [N][8], kff [N][2].  grad h / B' at x_{k+1} are carried from step k+1 (the reference
+// recomputes x_{k+1} = f(x_k, u_k) inside dubins_augmented_jacobian; it is the tape's X[k+1]).
+template <typename T>
+__device__ bool ilqr_backward(const DSpec<T>& s, const DCost<T>& c, T reg, const Col<T>& X,
+                              const Col<T>& U, const Col<T>& K, const Col<T>& kf,
+                              const Col<T>& Xr, int rf, const Col<T>& Ur) {
+  const int N = s.N;
+  T lxx[4], luu[2], pxx[4];
+  cost_diag(c, lxx, luu, pxx);
+  T xn0 = X.at(N, 4, 0), xn1 = X.at(N, 4, 1), xn2 = X.at(N, 4, 2), xnb = X.at(N, 4, 3);
+  T r0, r1, r2;
+  load_ref(c, Xr, rf, N, r0, r1, r2);
+  T d0, d1, d2;
+  deriv_dx(c, xn0, xn1, xn2, r0, r1, r2, d0, d1, d2);
+  Riccati<T> R;
+  R.Vx[0] = pxx[0] * d0;
+  R.Vx[1] = pxx[1] * d1;
+  R.Vx[2] = pxx[2] * d2;
+  R.Vx[3] = pxx[3] * xnb;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R.Vxx[i][j] = i == j ? pxx[i] : T(0);
+  T gxn, gyn;
+  T hn = h_grad(s, xn0, xn1, gxn, gyn);
+  T dBn = dbarrier_relaxed(s, hn);
+  bool ok = finite(R.Vx[0]) && finite(R.Vx[1]) && finite(R.Vx[2]) && finite(R.Vx[3]);
+  for (int k = N - 1; k >= 0; --k) {
+    T x0 = X.at(k, 4, 0), x1 = X.at(k, 4, 1), x2 = X.at(k, 4, 2), xb = X.at(k, 4, 3);
+    T u0 = U.at(k, 2, 0), u1 = U.at(k, 2, 1);
+    T q0, q1;
+    load_ref(c, Xr, rf, k, r0, r1, r2);
+    load_uref(c, Ur, k, q0, q1);
+    T sn, cs;
+    m_sincos(x2, &sn, &cs);
+    T gxk, gyk;
+    T hk = h_grad(s, x0, x1, gxk, gyk);
+    T dBk = dbarrier_relaxed(s, hk);
+    Jac<T> J = make_jac(s, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
+    deriv_dx(c, x0, x1, x2, r0, r1, r2, d0, d1, d2);
+    T lx[4] = {lxx[0] * d0, lxx[1] * d1, lxx[2] * d2, lxx[3] * xb};
+    T lu[2];
+    if (c.kind == DTMPC_COST_TRACK) {
+      lu[0] = luu[0] * (u0 - q0);
+      lu[1] = luu[1] * (u1 - q1);
+    } else {
+      lu[0] = luu[0] * u0;
+      lu[1] = luu[1] * u1;
+    }
+    T Kk[8], kk[2];
+    ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) K.at(k, 8, j) = Kk[j];
+    kf.at(k, 2, 0) = kk[0];
+    kf.at(k, 2, 1) = kk[1];
+    gxn = gxk;
+    gyn = gyk;
+    dBn = dBk;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ok = ok && finite(R.Vx[i]);
+  return ok;
+}
+
+// ---------------------------------------------------------------------------------------------
+// line search (core/ddp.py:256-301): all NA candidates advance together; returns the index of the
+// strictly smallest cost (first wins ties) or -1 if any candidate is non-finite.
+template <typename T, int NA>
+__device__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg,
+                           const T* x0, T Bc0, const Col<T>& X, const Col<T>& U, const Col<T>& K,
+                           const Col<T>& kf, const Col<T>& Xr, int rf, const Col<T>& Ur,
+                           T& bestJ) {
+  const int N = s.N;
+  T a0[NA], a1[NA], a2[NA], ab[NA], Bc[NA], J[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) {
+    a0[a] = x0[0];
+    a1[a] = x0[1];
+    a2[a] = x0[2];
+    ab[a] = x0[3];
+    Bc[a] = Bc0;
+    J[a] = T(0);
+  }
+  for (int k = 0; k < N; ++k) {
+    T X0 = X.at(k, 4, 0), X1 = X.at(k, 4, 1), X2 = X.at(k, 4, 2), X3 = X.at(k, 4, 3);
+    T V0 = U.at(k, 2, 0), V1 = U.at(k, 2, 1);
+    T Kk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Kk[j] = K.at(k, 8, j);
+    T k0 = kf.at(k, 2, 0), k1 = kf.at(k, 2, 1);
+    T r0, r1, r2, q0, q1;
+    load_ref(c, Xr, rf, k, r0, r1, r2);
+    load_uref(c, Ur, k, q0, q1);
+    T u0[NA], u1[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      T e0 = a0[a] - X0, e1 = a1[a] - X1, e2 = a2[a] - X2, e3 = ab[a] - X3;
+      T du0 = k0 + (Kk[0] * e0 + Kk[1] * e1 + Kk[2] * e2 + Kk[3] * e3);
+      T du1 = k1 + (Kk[4] * e0 + Kk[5] * e1 + Kk[6] * e2 + Kk[7] * e3);
+      T al = cfg.alphas[a];
+      u0[a] = clampv(V0 + al * du0, s.umin0, s.umax0);
+      u1[a] = clampv(V1 + al * du1, s.umin1, s.umax1);
+      J[a] = J[a] + stage_cost(c, a0[a], a1[a], a2[a], ab[a], u0[a], u1[a], r0, r1, r2, q0, q1);
+    }
+    fhat_vec<T, NA>(s, a0, a1, a2, ab, u0, u1, Bc);
+  }
+  T r0, r1, r2;
+  load_ref(c, Xr, rf, N, r0, r1, r2);
+  int best = 0;
+  bool ok = true;
+#pragma unroll
+  for (int a = 0; a < NA; ++a) {
+    J[a] = J[a] + term_cost(c, a0[a], a1[a], a2[a], ab[a], r0, r1, r2);
+    ok = ok && finite(J[a]);
+  }
+  bestJ = J[0];
+#pragma unroll
+  for (int a = 1; a < NA; ++a) {
+    if (J[a] < bestJ) {
+      bestJ = J[a];
+      best = a;
+    }
+  }
+  return ok ? best : -1;
+}
+
+// Materialise the chosen candidate in place: X, U <- rollout with step alpha (same arithmetic
+// as the candidate lane of line_search).  X[k+1] of the old tape is read before it is replaced.
+template <typename T>
+__device__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, const Col<T>& X,
+                                 const Col<T>& U, const Col<T>& K, const Col<T>& kf) {
+  const int N = s.N;
+  T s0[1] = {x0[0]}, s1[1] = {x0[1]}, s2[1] = {x0[2]}, sb[1] = {x0[3]}, Bc[1] = {Bc0};
+  T o0 = X.at(0, 4, 0), o1 = X.at(0, 4, 1), o2 = X.at(0, 4, 2), o3 = X.at(0, 4, 3);
+  for (int k = 0; k < N; ++k) {
+    T n0 = X.at(k + 1, 4, 0), n1 = X.at(k + 1, 4, 1), n2 = X.at(k + 1, 4, 2), n3 = X.at(k + 1, 4, 3);
+    T V0 = U.at(k, 2, 0), V1 = U.at(k, 2, 1);
+    T Kk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Kk[j] = K.at(k, 8, j);
+    T k0 = kf.at(k, 2, 0), k1 = kf.at(k, 2, 1);
+    T e0 = s0[0] - o0, e1 = s1[0] - o1, e2 = s2[0] - o2, e3 = sb[0] - o3;
+    T du0 = k0 + (Kk[0] * e0 + Kk[1] * e1 + Kk[2] * e2 + Kk[3] * e3);
+    T du1 = k1 + (Kk[4] * e0 + Kk[5] * e1 + Kk[6] * e2 + Kk[7] * e3);
+    T u0[1] = {clampv(V0 + al * du0, s.umin0, s.umax0)};
+    T u1[1] = {clampv(V1 + al * du1, s.umin1, s.umax1)};
+    U.at(k, 2, 0) = u0[0];
+    U.at(k, 2, 1) = u1[0];
+    fhat_vec<T, 1>(s, s0, s1, s2, sb, u0, u1, Bc);
+    X.at(k + 1, 4, 0) = s0[0];
+    X.at(k + 1, 4, 1) = s1[0];
+    X.at(k + 1, 4, 2) = s2[0];
+    X.at(k + 1, 4, 3) = sb[0];
+    o0 = n0;
+    o1 = n1;
+    o2 = n2;
+    o3 = n3;
+  }
+}
+
+// rollout core/ddp.py:89-99 (U used as stored)
+template <typename T>
+__device__ void rollout_traj(const DSpec<T>& s, const T* x0, const Col<T>& X, const Col<T>& U) {
+  const int N = s.N;
+  T s0[1] = {x0[0]}, s1[1] = {x0[1]}, s2[1] = {x0[2]}, sb[1] = {x0[3]};
+  T Bc[1] = {barrier_of_state(s, x0[0], x0[1])};
+  X.at(0, 4, 0) = s0[0];
+  X.at(0, 4, 1) = s1[0];
+  X.at(0, 4, 2) = s2[0];
+  X.at(0, 4, 3) = sb[0];
+  for (int k = 0; k < N; ++k) {
+    T u0[1] = {U.at(k, 2, 0)}, u1[1] = {U.at(k, 2, 1)};
+    fhat_vec<T, 1>(s, s0, s1, s2, sb, u0, u1, Bc);
+    X.at(k + 1, 4, 0) = s0[0];
+    X.at(k + 1, 4, 1) = s1[0];
+    X.at(k + 1, 4, 2) = s2[0];
+    X.at(k + 1, 4, 3) = sb[0];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// iLQR for one trajectory (core/ddp.py:102-307).  U: in V_init, out V*.  X: out X*.
+// K/kf: scratch + gains of the last backward pass.  Returns DTMPC_ST_* bits.
+template <typename T, int NA>
+__device__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, const T* x0,
+                         const Col<T>& X, const Col<T>& U, const Col<T>& K, const Col<T>& kf,
+                         const Col<T>& Xr, int rf, const Col<T>& Ur, int& iters) {
+  const int N = s.N;
+  // V = clamp(V_init); X = rollout(x0, V)   (:127-131)
+  for (int k = 0; k < N; ++k) {
+    U.at(k, 2, 0) = clampv(U.at(k, 2, 0), s.umin0, s.umax0);
+    U.at(k, 2, 1) = clampv(U.at(k, 2, 1), s.umin1, s.umax1);
+  }
+  rollout_traj(s, x0, X, U);
+  T Bc0 = barrier_of_state(s, x0[0], x0[1]);
+  bool have_prev = false;
+  T prev = T(0);
+  iters = 0;
+  for (int it = 0; it < cfg.max_iter; ++it) {
+    iters = it + 1;
+    if (!ilqr_backward(s, c, cfg.reg, X, U, K, kf, Xr, rf, Ur)) return DTMPC_ST_NONFINITE;
+    T bestJ;
+    int best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, K, kf, Xr, rf, Ur, bestJ);
+    if (best < 0) return DTMPC_ST_NONFINITE;
+    T al = cfg.alphas[best];
+    if (al != T(0)) commit_candidate(s, al, x0, Bc0, X, U, K, kf);
+    // :303-305
+    if (have_prev && m_abs(prev - bestJ) < cfg.tol) break;
+    have_prev = true;
+    prev = bestJ;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// DDP sensitivity (core/ddp.py:317-427) with the paper upper loss (core/tube_mpc.py:932-944):
+//   g_x(k) = [2 (x_k - xbar_k), 2 b_k], g_u = 0, same at k = N.
+// AB scratch [N][10]: a02 a12 a30 a31 a32 b00 b10 b30 b31 act(=act0 + 2 act1).
+// VV scratch [N+1][20] (LAMBDA): V_xx (16) and tilde V_x (4) for delta_lambda.
+// GRAD: accumulate the upper loss and the analytic DOC gradient (core/tube_mpc.py:915-976) into
+// acc[7] = L, gQ(3), gR(2), gqb with du = U - Ur.
+template <typename T, bool LAMBDA, bool OUT, bool GRAD>
+__device__ int sens_traj(const DSpec<T>& s, const DCost<T>& c, const Col<T>& X, const Col<T>& U,
+                         const Col<T>& Xr, int rf, const Col<T>& Ur, const Col<T>& Xb, int rfb,
+                         const Col<T>& K, const Col<T>& kf, const Col<T>& AB, const Col<T>& VV,
+                         const Col<T>& dX, const Col<T>& dU, const Col<T>& dL, T* acc) {
+  const int N = s.N;
+  T lxx[4], luu[2], pxx[4];
+  cost_diag(c, lxx, luu, pxx);
+  const T reg = T(1e-9);
+  Riccati<T> R;  // R.Vx holds tilde V_x
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R.Vxx[i][j] = i == j ? pxx[i] : T(0);
+  T xn0 = X.at(N, 4, 0), xn1 = X.at(N, 4, 1), xnb = X.at(N, 4, 3);
+  R.Vx[0] = T(2) * (xn0 - Xb.at(N, rfb, 0));
+  R.Vx[1] = T(2) * (xn1 - Xb.at(N, rfb, 1));
+  R.Vx[2] = T(2) * (X.at(N, 4, 2) - Xb.at(N, rfb, 2));
+  R.Vx[3] = T(2) * xnb;
+  if (LAMBDA) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) VV.at(N, 20, 4 * i + j) = R.Vxx[i][j];
+      VV.at(N, 20, 16 + i) = R.Vx[i];
+    }
+  }
+  T gxn, gyn;
+  T hn = h_grad(s, xn0, xn1, gxn, gyn);
+  T dBn = dbarrier_relaxed(s, hn);
+  for (int k = N - 1; k >= 0; --k) {
+    T x0 = X.at(k, 4, 0), x1 = X.at(k, 4, 1), x2 = X.at(k, 4, 2), xb = X.at(k, 4, 3);
+    T u0 = U.at(k, 2, 0), u1 = U.at(k, 2, 1);
+    T sn, cs;
+    m_sincos(x2, &sn, &cs);
+    T gxk, gyk;
+    T hk = h_grad(s, x0, x1, gxk, gyk);
+    T dBk = dbarrier_relaxed(s, hk);
+    Jac<T> J = make_jac(s, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
+    gxn = gxk;
+    gyn = gyk;
+    dBn = dBk;
+    const T(&V)[4][4] = R.Vxx;
+    T P[4][4];  // A^T V_xx
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      P[0][j] = V[0][j] + J.a30 * V[3][j];
+      P[1][j] = V[1][j] + J.a31 * V[3][j];
+      P[2][j] = J.a02 * V[0][j] + J.a12 * V[1][j] + V[2][j] + J.a32 * V[3][j];
+      P[3][j] = J.g * V[3][j];
+    }
+    T Qxx[4][4], Qxu[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Qxx[i][0] = P[i][0] + P[i][3] * J.a30;
+      Qxx[i][1] = P[i][1] + P[i][3] * J.a31;
+      Qxx[i][2] = P[i][0] * J.a02 + P[i][1] * J.a12 + P[i][2] + P[i][3] * J.a32;
+      Qxx[i][3] = P[i][3] * J.g;
+      Qxx[i][i] = lxx[i] + Qxx[i][i];
+      // Q_xu = l_ux^T + A^T V_xx B   (:380)
+      Qxu[i][0] = P[i][0] * J.b00 + P[i][1] * J.b10 + P[i][3] * J.b30;
+      Qxu[i][1] = P[i][2] * J.b21 + P[i][3] * J.b31;
+    }
+    T S[2][4];  // B^T V_xx
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      S[0][j] = J.b00 * V[0][j] + J.b10 * V[1][j] + J.b30 * V[3][j];
+      S[1][j] = J.b21 * V[2][j] + J.b31 * V[3][j];
+    }
+    T Qux[2][4], Quu[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      Qux[a][0] = S[a][0] + S[a][3] * J.a30;
+      Qux[a][1] = S[a][1] + S[a][3] * J.a31;
+      Qux[a][2] = S[a][0] * J.a02 + S[a][1] * J.a12 + S[a][2] + S[a][3] * J.a32;
+      Qux[a][3] = S[a][3] * J.g;
+      Quu[a][0] = S[a][0] * J.b00 + S[a][1] * J.b10 + S[a][3] * J.b30;
+      Quu[a][1] = S[a][2] * J.b21 + S[a][3] * J.b31;
+    }
+    Quu[0][0] = luu[0] + Quu[0][0];
+    Quu[1][1] = luu[1] + Quu[1][1];
+    const T* tv = R.Vx;
+    T tQu0 = J.b00 * tv[0] + J.b10 * tv[1] + J.b30 * tv[3];
+    T tQu1 = J.b21 * tv[2] + J.b31 * tv[3];
+    T tQx[4];
+    tQx[0] = T(2) * (x0 - Xb.at(k, rfb, 0)) + (tv[0] + J.a30 * tv[3]);
+    tQx[1] = T(2) * (x1 - Xb.at(k, rfb, 1)) + (tv[1] + J.a31 * tv[3]);
+    tQx[2] = T(2) * (x2 - Xb.at(k, rfb, 2)) + (J.a02 * tv[0] + J.a12 * tv[1] + tv[2] + J.a32 * tv[3]);
+    tQx[3] = T(2) * xb + J.g * tv[3];
+    // active set (core/control.py:66-70)
+    bool act0 = (u0 <= s.umin0 + s.active_tol) || (u0 >= s.umax0 - s.active_tol);
+    bool act1 = (u1 <= s.umin1 + s.active_tol) || (u1 >= s.umax1 - s.active_tol);
+    T m00 = Quu[0][0] + reg, m11 = Quu[1][1] + reg;
+    LU2<T> f = lu2(m00, Quu[0][1], Quu[1][0], m11);
+    T Kk[8], kk[2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      T y0, y1;
+      solve_reduced(f, m00, m11, act0, act1, Qux[0][j], Qux[1][j], y0, y1);
+      Kk[j] = -y0;
+      Kk[4 + j] = -y1;
+    }
+    {
+      T y0, y1;
+      solve_reduced(f, m00, m11, act0, act1, tQu0, tQu1, y0, y1);
+      kk[0] = -y0;
+      kk[1] = -y1;
+    }
+    // tilde V_x = tilde Q_x + Q_xu k ; V_xx = Q_xx + Q_xu K   (:403-404)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      R.Vx[i] = tQx[i] + (Qxu[i][0] * kk[0] + Qxu[i][1] * kk[1]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) R.Vxx[i][j] = Qxx[i][j] + (Qxu[i][0] * Kk[j] + Qxu[i][1] * Kk[4 + j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) K.at(k, 8, j) = Kk[j];
+    kf.at(k, 2, 0) = kk[0];
+    kf.at(k, 2, 1) = kk[1];
+    AB.at(k, 10, 0) = J.a02;
+    AB.at(k, 10, 1) = J.a12;
+    AB.at(k, 10, 2) = J.a30;
+    AB.at(k, 10, 3) = J.a31;
+    AB.at(k, 10, 4) = J.a32;
+    AB.at(k, 10, 5) = J.b00;
+    AB.at(k, 10, 6) = J.b10;
+    AB.at(k, 10, 7) = J.b30;
+    AB.at(k, 10, 8) = J.b31;
+    AB.at(k, 10, 9) = T((act0 ? 1 : 0) + (act1 ? 2 : 0));
+    if (LAMBDA) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) VV.at(k, 20, 4 * i + j) = R.Vxx[i][j];
+        VV.at(k, 20, 16 + i) = R.Vx[i];
+      }
+    }
+  }
+  // forward (:413-425)
+  T d[4] = {T(0), T(0), T(0), T(0)};
+  T L1 = T(0), L2 = T(0), gQ0 = T(0), gQ1 = T(0), gQ2 = T(0), gR0 = T(0), gR1 = T(0), gqb = T(0);
+  bool ok = true;
+  const T g = s.gamma, dt = s.dt;
+  for (int k = 0; k < N; ++k) {
+    T Kk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Kk[j] = K.at(k, 8, j);
+    T k0 = kf.at(k, 2, 0), k1 = kf.at(k, 2, 1);
+    T a02 = AB.at(k, 10, 0), a12 = AB.at(k, 10, 1), a30 = AB.at(k, 10, 2), a31 = AB.at(k, 10, 3),
+      a32 = AB.at(k, 10, 4), b00 = AB.at(k, 10, 5), b10 = AB.at(k, 10, 6), b30 = AB.at(k, 10, 7),
+      b31 = AB.at(k, 10, 8);
+    int act = (int)AB.at(k, 10, 9);
+    T v0 = (act & 1) ? T(0) : k0 + (Kk[0] * d[0] + Kk[1] * d[1] + Kk[2] * d[2] + Kk[3] * d[3]);
+    T v1 = (act & 2) ? T(0) : k1 + (Kk[4] * d[0] + Kk[5] * d[1] + Kk[6] * d[2] + Kk[7] * d[3]);
+    if (LAMBDA) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        T acc1 = VV.at(k, 20, 4 * i + 0) * d[0] + VV.at(k, 20, 4 * i + 1) * d[1] +
+                 VV.at(k, 20, 4 * i + 2) * d[2] + VV.at(k, 20, 4 * i + 3) * d[3];
+        dL.at(k, 4, i) = VV.at(k, 20, 16 + i) + acc1;
+      }
+    }
+    if (OUT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dX.at(k, 4, i) = d[i];
+      dU.at(k, 2, 0) = v0;
+      dU.at(k, 2, 1) = v1;
+    }
+    if (GRAD) {
+      T e0 = X.at(k, 4, 0) - Xb.at(k, rfb, 0);
+      T e1 = X.at(k, 4, 1) - Xb.at(k, rfb, 1);
+      T e2 = X.at(k, 4, 2) - Xb.at(k, rfb, 2);
+      T bb = X.at(k, 4, 3);
+      T w0 = U.at(k, 2, 0) - Ur.at(k, 2, 0);
+      T w1 = U.at(k, 2, 1) - Ur.at(k, 2, 1);
+      L1 += e0 * e0 + e1 * e1 + e2 * e2;
+      L2 += bb * bb;
+      gQ0 += T(2) * e0 * d[0];
+      gQ1 += T(2) * e1 * d[1];
+      gQ2 += T(2) * e2 * d[2];
+      gR0 += T(2) * w0 * v0;
+      gR1 += T(2) * w1 * v1;
+      gqb += T(2) * bb * d[3];
+    }
+    // delta x_{k+1} = A delta x_k + B delta u_k
+    T n0 = (d[0] + a02 * d[2]) + b00 * v0;
+    T n1 = (d[1] + a12 * d[2]) + b10 * v0;
+    T n2 = d[2] + dt * v1;
+    T n3 = (a30 * d[0] + a31 * d[1] + a32 * d[2] + g * d[3]) + (b30 * v0 + b31 * v1);
+    d[0] = n0;
+    d[1] = n1;
+    d[2] = n2;
+    d[3] = n3;
+  }
+  if (LAMBDA) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      T acc1 = VV.at(N, 20, 4 * i + 0) * d[0] + VV.at(N, 20, 4 * i + 1) * d[1] +
+               VV.at(N, 20, 4 * i + 2) * d[2] + VV.at(N, 20, 4 * i + 3) * d[3];
+      dL.at(N, 4, i) = VV.at(N, 20, 16 + i) + acc1;
+    }
+  }
+  if (OUT) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dX.at(N, 4, i) = d[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ok = ok && finite(d[i]);
+  if (GRAD) {
+    T e0 = X.at(N, 4, 0) - Xb.at(N, rfb, 0);
+    T e1 = X.at(N, 4, 1) - Xb.at(N, rfb, 1);
+    T e2 = X.at(N, 4, 2) - Xb.at(N, rfb, 2);
+    T bb = X.at(N, 4, 3);
+    L1 += e0 * e0 + e1 * e1 + e2 * e2;
+    L2 += bb * bb;
+    acc[0] = L1 + L2;
+    acc[1] = gQ0 + T(2) * e0 * d[0];
+    acc[2] = gQ1 + T(2) * e1 * d[1];
+    acc[3] = gQ2 + T(2) * e2 * d[2];
+    acc[4] = gR0;
+    acc[5] = gR1;
+    acc[6] = gqb + T(2) * bb * d[3];
+    ok = ok && finite(acc[1]) && finite(acc[4]) && finite(acc[5]);
+  }
+  return ok ? 0 : DTMPC_ST_NONFINITE;
+}
+
+}  // namespace dtmpc

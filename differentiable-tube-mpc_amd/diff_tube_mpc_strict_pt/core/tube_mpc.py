@@ -1,0 +1,267 @@
+"""Batched differentiable tube MPC on MI355X (HIP), Algorithm 2 of the paper.
+
+* :class:`TubeMPC` — NEW batched entry (the reference has no such class): B independent
+  closed loops share the adaptive ancillary weights theta = (Qa, Ra, qba).  One call of
+  :meth:`TubeMPC.step` = one closed-loop step for every trajectory (core/tube_mpc.py:803-1023):
+  nominal iLQR -> ancillary iLQR -> upper loss -> DDP sensitivity -> DOC gradient -> plant step ->
+  warm-start shift, all inside one fused HIP kernel; then a fixed-order reduction of the
+  per-workgroup gradient sums, a cross-rank all-reduce (RCCL) when the batch is sharded, and the
+  momentum/projection update of theta (core/tube_mpc.py:978-984) with the batch-mean gradient.
+  With B = 1 this is exactly the reference's loop body.
+* :func:`run_closed_loop_experiment` — signature- and output-compatible with the reference
+  (core/tube_mpc.py:40), for the configured paper mode (core/tube_mpc.py:666-1048).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from dataclasses import dataclass
+from typing import Any, Dict, Optional, Tuple
+
+import numpy as np
+import torch
+from torch import Tensor
+
+from .. import _abi, _lib
+from .ddp import _dtype_code, raise_for_status
+from .problem import PaperSetup, paper_setup_from_config
+
+__all__ = ["ExperimentTrajectories", "TubeMPC", "run_closed_loop_experiment", "shard_range", "allreduce_sums"]
+
+
+@dataclass
+class ExperimentTrajectories:
+    """core/tube_mpc.py:27-37"""
+
+    x_real: list
+    u_real: list
+    x_bar: list
+    u_bar: list
+    loss: list
+    b_real: list
+    Qa_history: list
+    Ra_history: list
+    qba_history: list
+
+
+def shard_range(global_batch: int, rank: int, world_size: int) -> Tuple[int, int]:
+    """Contiguous global-index slice [lo, hi) of trajectories owned by `rank`."""
+    if world_size < 1 or not (0 <= rank < world_size):
+        raise ValueError("bad rank / world_size")
+    base, rem = divmod(global_batch, world_size)
+    lo = rank * base + min(rank, rem)
+    hi = lo + base + (1 if rank < rem else 0)
+    return lo, hi
+
+
+def allreduce_sums(sums: Tensor, group=None) -> Tensor:
+    """Sum the [L, gQ(3), gR(2), gqb, 0] vector over ranks (RCCL on HIP devices, gloo on CPU)."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+    return sums
+
+
+class TubeMPC:
+    """Device-resident batched closed loop.
+
+    Args:
+      setup: :class:`PaperSetup` (or a config dict for :func:`paper_setup_from_config`).
+      batch: trajectories owned by this process.
+      device: HIP device.
+      dtype: torch.float32 (default, the benchmark precision) or torch.float64.
+      disturbance: "philox" (device counter-based RNG keyed by global index and step) or "injected"
+        (pass w to :meth:`step`).
+      global_offset / global_batch: position of this shard in the global batch (multi-GPU).
+      write_log: keep the per-step record (x, u, xbar, ubar, b, L) on device.
+    """
+
+    def __init__(self, setup, *, batch: int, device="cuda", dtype=torch.float32, disturbance: str = "philox",
+                 seed: int = 0, global_offset: int = 0, global_batch: Optional[int] = None, process_group=None,
+                 write_log: bool = False):
+        if isinstance(setup, dict):
+            setup = paper_setup_from_config(setup)
+        self.setup: PaperSetup = setup
+        self.B = int(batch)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("TubeMPC runs on a HIP device; there is no CPU fallback")
+        self.dtype = dtype
+        self.global_offset = int(global_offset)
+        self.global_batch = int(global_batch) if global_batch is not None else self.B
+        self.group = process_group
+        self.lib = _lib.load()
+        p = setup.problem
+        self.N = N = p.horizon
+        if setup.ilqr_nom.line_search_alphas != setup.ilqr_aux.line_search_alphas:
+            raise ValueError("nominal and ancillary solves must share the line-search alphas")
+        self._dt = _dtype_code(torch.empty(0, dtype=dtype))
+        self.spec = p.to_c()
+        cfg = _abi.DtmpcTubeCfg()
+        cfg.nominal = setup.nominal_cost.to_c()
+        cfg.nom_ilqr = setup.ilqr_nom.to_c()
+        cfg.aux_ilqr = setup.ilqr_aux.to_c()
+        if disturbance not in ("philox", "injected"):
+            raise ValueError("disturbance must be 'philox' or 'injected'")
+        cfg.disturbance = 1 if disturbance == "philox" else 0
+        cfg.write_log = 1 if write_log else 0
+        cfg.seed = int(seed) & ((1 << 64) - 1)
+        for f in range(3):
+            cfg.w_low[f] = float(setup.w_low[f])
+            cfg.w_high[f] = float(setup.w_high[f])
+        self.cfg = cfg
+        self.adapt = setup.adapt.to_c()
+        kw = dict(dtype=dtype, device=self.device)
+        B = self.B
+        self.x = torch.zeros(3, B, **kw)
+        self.b = torch.zeros(B, **kw)
+        self.xbar = torch.zeros(3, B, **kw)
+        self.bbar = torch.zeros(B, **kw)
+        self.Xnom = torch.zeros(N + 1, 4, B, **kw)
+        self.Unom = torch.zeros(N, 2, B, **kw)
+        self.Xaux = torch.zeros(N + 1, 4, B, **kw)
+        self.Uaux = torch.zeros(N, 2, B, **kw)
+        self.work = torch.empty(self.lib.dtmpc_tube_workspace_bytes(self._dt, N, B), dtype=torch.uint8,
+                                device=self.device)
+        self.n_partials = int(self.lib.dtmpc_tube_partials_count(B))
+        self.partials = torch.zeros(self.n_partials, 8, **kw)
+        self.sums = torch.zeros(8, **kw)
+        self.theta = torch.tensor(setup.theta0, **kw)
+        self.vel = torch.zeros(6, **kw)
+        self.status = torch.zeros(B, dtype=torch.int32, device=self.device)
+        self.iters = torch.zeros(2, B, dtype=torch.int32, device=self.device)
+        self.log = torch.zeros(12, B, **kw) if write_log else None
+        self.t = 0
+        st = _abi.DtmpcTubeState()
+        st.x, st.b, st.xbar, st.bbar = (t.data_ptr() for t in (self.x, self.b, self.xbar, self.bbar))
+        st.Xnom, st.Unom, st.Xaux, st.Uaux = (t.data_ptr() for t in (self.Xnom, self.Unom, self.Xaux, self.Uaux))
+        st.work = self.work.data_ptr()
+        st.theta = self.theta.data_ptr()
+        st.partials = self.partials.data_ptr()
+        st.log = self.log.data_ptr() if self.log is not None else None
+        st.status = self.status.data_ptr()
+        st.iters = self.iters.data_ptr()
+        self.state = st
+
+    # -----------------------------------------------------------------------------------------
+    def reset(self, x0: Tensor, U_nom0: Optional[Tensor] = None, U_aux0: Optional[Tensor] = None) -> None:
+        """x0 [B, 3]: plant and nominal start at x0, b0 = B(h(x0)) (core/tube_mpc.py:770-779);
+        warm starts default to zero; theta and momentum restart from the setup."""
+        if x0.shape != (self.B, 3):
+            raise ValueError(f"x0 must be [{self.B}, 3]")
+        xs = x0.to(device=self.device, dtype=self.dtype).t().contiguous()
+        self.x.copy_(xs)
+        self.xbar.copy_(xs)
+        _lib.check(self.lib.dtmpc_dbas_init(self._dt, C.byref(self.spec), self.B, self.x.data_ptr(),
+                                            self.b.data_ptr(), self._stream()), "dtmpc_dbas_init")
+        self.bbar.copy_(self.b)
+        self.Unom.zero_()
+        self.Uaux.zero_()
+        if U_nom0 is not None:
+            self.Unom.copy_(U_nom0.to(self.Unom).permute(1, 2, 0))
+        if U_aux0 is not None:
+            self.Uaux.copy_(U_aux0.to(self.Uaux).permute(1, 2, 0))
+        self.theta.copy_(torch.tensor(self.setup.theta0, dtype=self.dtype))
+        self.vel.zero_()
+        self.status.zero_()
+        self.t = 0
+
+    def _stream(self) -> int:
+        return int(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def step(self, w: Optional[Tensor] = None) -> None:
+        """One closed-loop step for the whole batch (asynchronous on the current stream)."""
+        wp = None
+        if self.cfg.disturbance == 0:
+            if w is None or w.shape != (self.B, 3):
+                raise ValueError(f"injected disturbance w must be [{self.B}, 3]")
+            self._w = w.to(device=self.device, dtype=self.dtype).t().contiguous()
+            wp = self._w.data_ptr()
+        s = self._stream()
+        _lib.check(self.lib.dtmpc_tube_step(self._dt, C.byref(self.spec), C.byref(self.cfg), self.B,
+                                            self.global_offset, self.t, C.byref(self.state), wp, s),
+                   "dtmpc_tube_step")
+        _lib.check(self.lib.dtmpc_partials_reduce(self._dt, self.n_partials, self.partials.data_ptr(),
+                                                  self.sums.data_ptr(), s), "dtmpc_partials_reduce")
+        allreduce_sums(self.sums, self.group)
+        _lib.check(self.lib.dtmpc_theta_update(self._dt, C.byref(self.adapt), 1.0 / self.global_batch,
+                                               self.sums.data_ptr(), self.theta.data_ptr(), self.vel.data_ptr(), s),
+                   "dtmpc_theta_update")
+        self.t += 1
+
+    def check(self) -> None:
+        raise_for_status(self.status, "tube step")
+
+    # convenience views (trajectory-major copies)
+    @property
+    def loss_mean(self) -> float:
+        return float(self.sums[0]) / self.global_batch
+
+    def nominal_tape(self):
+        return self.Xnom.permute(2, 0, 1), self.Unom.permute(2, 0, 1)
+
+
+# ---------------------------------------------------------------------------------------------
+def run_closed_loop_experiment(cfg: Dict[str, Any], *, device: torch.device, run_dir: str) -> Dict[str, Any]:
+    """Drop-in for core/tube_mpc.py:40 in the configured paper mode (core/tube_mpc.py:666-1048).
+
+    The disturbance is drawn exactly as the reference draws it (torch.rand_like on ``device`` with
+    the global generator, core/systems/dubins.py:59-67), then injected into the fused HIP step, so a
+    seeded run consumes the same random stream as the reference."""
+    system_cfg = cfg["system"]
+    if system_cfg["name"] != "dubins":
+        raise NotImplementedError("Only dubins is wired in the skeleton; other systems are added next.")
+    paper_mode = bool(cfg.get("paper_dubins_mode", True))
+    adapt_nominal = bool(cfg.get("adaptation", {}).get("adapt_nominal", False))
+    if not paper_mode or adapt_nominal:
+        raise NotImplementedError(
+            "the general (softplus-parameterised, adapt_nominal) IFT path of core/tube_mpc.py:40-663 is not "
+            "part of this build's hot path yet (SURVEY.md §8f-1); use the paper mode")
+    device = torch.device(device)
+    setup = paper_setup_from_config(cfg)
+    dtype = torch.float64 if setup.use_float64 else torch.float32
+    H = setup.task_horizon
+    mpc = TubeMPC(setup, batch=1, device=device, dtype=dtype, disturbance="injected", write_log=True)
+    x0 = torch.tensor([list(setup.x0)], dtype=dtype, device=device)
+    mpc.reset(x0)
+    low = torch.tensor(setup.w_low, device=device, dtype=dtype)
+    high = torch.tensor(setup.w_high, device=device, dtype=dtype)
+    logs = torch.zeros(H, 12, dtype=dtype, device=device)
+    thetas = torch.zeros(H, 6, dtype=dtype, device=device)
+    probe = torch.empty(1, 3, device=device, dtype=dtype)
+    for t in range(H):
+        if (t % 25) == 0:
+            print(f"[step {t}/{H}] running...", flush=True)
+        w = low + (high - low) * torch.rand_like(probe)
+        mpc.step(w)
+        logs[t].copy_(mpc.log[:, 0])
+        thetas[t].copy_(mpc.theta)
+    mpc.check()
+    lg = logs.cpu().numpy()
+    th = thetas.cpu().numpy()
+    traj = ExperimentTrajectories(
+        x_real=list(lg[:, 0:3]), u_real=list(lg[:, 3:5]), x_bar=list(lg[:, 5:8]), u_bar=list(lg[:, 8:10]),
+        loss=[float(v) for v in lg[:, 11]], b_real=list(lg[:, 10]), Qa_history=list(th[:, 0:3]),
+        Ra_history=list(th[:, 3:5]), qba_history=[float(v) for v in th[:, 5]])
+    os.makedirs(run_dir, exist_ok=True)
+    np.save(os.path.join(run_dir, "x_real.npy"), np.stack(traj.x_real, axis=0))
+    np.save(os.path.join(run_dir, "u_real.npy"), np.stack(traj.u_real, axis=0))
+    np.save(os.path.join(run_dir, "x_bar.npy"), np.stack(traj.x_bar, axis=0))
+    np.save(os.path.join(run_dir, "u_bar.npy"), np.stack(traj.u_bar, axis=0))
+    np.save(os.path.join(run_dir, "b_real.npy"), np.stack(traj.b_real, axis=0))
+    np.save(os.path.join(run_dir, "loss.npy"), np.asarray(traj.loss, dtype=np.float64))
+    np.save(os.path.join(run_dir, "Qa_history.npy"), np.stack(traj.Qa_history, axis=0))
+    np.save(os.path.join(run_dir, "Ra_history.npy"), np.stack(traj.Ra_history, axis=0))
+    np.save(os.path.join(run_dir, "qba_history.npy"), np.asarray(traj.qba_history, dtype=np.float64))
+    summary = {
+        "system": "dubins",
+        "H": H,
+        "N": setup.problem.horizon,
+        "final_state": np.asarray(traj.x_real[-1]).tolist(),
+        "final_barrier_state": float(np.array(traj.b_real[-1]).reshape(-1)[0]),
+        "final_loss": float(traj.loss[-1]),
+        "note": "Dubins run aligned to paper: nominal fixed, ancillary adapts, alpha=0, gamma=0.",
+    }
+    return {"summary": summary}

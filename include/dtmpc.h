@@ -1,0 +1,249 @@
+/*
+ * dtmpc.h — C ABI of the MI355X-native batched differentiable tube-MPC hot path.
+ *
+ * The reference (lmcggg/differentiable-tube-mpc) has no FFI: its solver boundary is a
+ * Python-closure boundary (core/ddp.py:102-117, core/ddp.py:317-329) fed by closures built in
+ * core/tube_mpc.py:814-957.  This header replaces those closures with a TYPED problem
+ * specification (Dubins + DBaS barrier state + circle obstacles + diagonal quadratic costs + box
+ * controls) that the HIP kernels in libdtmpc.so consume for a whole batch of independent
+ * trajectories at once.  Every entry point below names the reference function it replaces.
+ *
+ * Conventions (all entry points):
+ *   - dtype: DTMPC_F32 or DTMPC_F64; every `void*` array argument holds that scalar type.
+ *   - Batched arrays are SoA "step-major, trajectory-minor": element (k, f, i) of an array with
+ *     F fields per step lives at index (k*F + f)*B + i.  Trajectory i of the batch is one
+ *     independent copy of the reference's single-trajectory problem.
+ *   - All array pointers are DEVICE pointers owned by the caller; nothing is allocated inside
+ *     (scratch comes from caller-provided workspaces sized by the *_workspace_bytes queries).
+ *   - Launches are asynchronous on the given hipStream_t (`stream`, NULL = default stream);
+ *     entry points are re-entrant across streams.
+ *   - Return value: DTMPC_OK or DTMPC_ERR_BAD_ARG / DTMPC_ERR_HIP for launch-time failures.
+ *     Numerical failures are reported per trajectory through `status` words (bit flags
+ *     DTMPC_ST_*), which the host maps to the reference's exceptions (FloatingPointError for
+ *     non-finite values, core/ddp.py:138-159; RuntimeError when line search yields nothing,
+ *     core/ddp.py:298-299).
+ */
+#ifndef DTMPC_H
+#define DTMPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DTMPC_ABI_VERSION 1
+#define DTMPC_MAX_OBS 16
+#define DTMPC_MAX_ALPHAS 8
+#define DTMPC_MAX_HORIZON 512
+
+/* scalar type of the arrays */
+enum { DTMPC_F32 = 0, DTMPC_F64 = 1 };
+
+/* obstacle aggregation for the safety function h (core/systems/dubins_aug_jac.py:96-112) */
+enum {
+  DTMPC_OBS_SMOOTHMIN = 0, /* h = -(1/beta) LSE(-beta h_i), dubins_obstacles.py:41-92 */
+  DTMPC_OBS_MIN = 1,       /* h = min_i h_i, argmin subgradient, dubins_obstacles.py:95-117 */
+  DTMPC_OBS_SINGLE = 2,    /* one circle (obstacle 0), dubins_obstacles.py:16-38 */
+  DTMPC_OBS_NONE = 3       /* h = 1 (run_nominal.py:256) */
+};
+
+/* barrier used in the DBaS dynamics b' = B(h(f(x,u))) - gamma (B(h(x)) - b)  (core/barrier.py:75-108).
+ * The linearisation always differentiates the relaxed inverse barrier, exactly as the
+ * reference does (core/systems/dubins_aug_jac.py:116-122). */
+enum { DTMPC_BARRIER_INVERSE = 0, DTMPC_BARRIER_LOG = 1 };
+
+/* stage/terminal cost family */
+enum {
+  DTMPC_COST_TARGET = 0, /* nominal: sum Q (x-x*)^2 + R u^2 + qb b^2 (core/tube_mpc.py:823-842) */
+  DTMPC_COST_TRACK = 1   /* ancillary: sum Q (x-xref_k)^2 + R (u-uref_k)^2 + qb b^2 (core/tube_mpc.py:875-894) */
+};
+
+/* return codes */
+enum {
+  DTMPC_OK = 0,
+  DTMPC_ERR_BAD_ARG = 3,
+  DTMPC_ERR_HIP = 4
+};
+
+/* per-trajectory status bits */
+enum {
+  DTMPC_ST_NONFINITE = 1,    /* FloatingPointError in the reference */
+  DTMPC_ST_NO_CANDIDATE = 2  /* RuntimeError("iLQR line search failed ...") */
+};
+
+/* Problem specification: system + environment + DBaS (core/tube_mpc.py:680-721). */
+typedef struct dtmpc_spec {
+  int32_t horizon;          /* N (configs/dubins.yaml:13) */
+  int32_t n_obstacles;      /* M <= DTMPC_MAX_OBS */
+  int32_t obs_aggregation;  /* DTMPC_OBS_* */
+  int32_t barrier_type;     /* DTMPC_BARRIER_* */
+  double dt;                /* DubinsConfig.dt (core/systems/dubins.py:14) */
+  double u_min[2];          /* BoxClampControl.u_min (core/control.py:56) */
+  double u_max[2];
+  double active_tol;        /* BoxClampControl.active_tol = 1e-8 (core/control.py:59) */
+  double obs_beta;          /* smooth-min temperature (configs/dubins.yaml:59) */
+  double obs_cx[DTMPC_MAX_OBS];
+  double obs_cy[DTMPC_MAX_OBS];
+  double obs_r[DTMPC_MAX_OBS];
+  double dbas_alpha;        /* DBaSConfig.alpha (core/barrier.py:29) */
+  double dbas_gamma;        /* DBaSConfig.gamma, in [-1, 1] */
+  double dbas_eps;          /* DBaSConfig.eps */
+} dtmpc_spec;
+
+/* Quadratic stage/terminal cost (core/cost_derivs.py:58-146 + caller overrides in
+ * core/tube_mpc.py:837-842, 890-894 and run_nominal.py:297-324). */
+typedef struct dtmpc_cost {
+  int32_t kind;             /* DTMPC_COST_* */
+  int32_t wrap_angle;       /* 1: heading error wrapped to (-pi, pi] (run_nominal.py:32-34, 297-324) */
+  double Q[3];
+  double R[2];
+  double Qf[3];             /* terminal weight; the paper ancillary passes Qf = Q (core/tube_mpc.py:885, 891) */
+  double qb;
+  double target[3];         /* DTMPC_COST_TARGET only */
+} dtmpc_cost;
+
+/* ILQRConfig (core/ddp.py:12-20) */
+typedef struct dtmpc_ilqr_cfg {
+  int32_t max_iter;
+  int32_t n_alphas;         /* <= DTMPC_MAX_ALPHAS */
+  double tol;               /* early exit when |J_prev - J_best| < tol; tol < 0 = fixed iterations */
+  double reg;               /* Quu regulariser (core/ddp.py:136, 239) */
+  double alphas[DTMPC_MAX_ALPHAS];
+} dtmpc_ilqr_cfg;
+
+/* Online adaptation of the ancillary weights (core/tube_mpc.py:746-752, 978-984). */
+typedef struct dtmpc_adapt_cfg {
+  double lr_eta;
+  double momentum;
+  double q_min;             /* Qa >= 0 */
+  double r_min;             /* Ra >= 1e-4 */
+  double qb_min, qb_max;    /* qba in [0, 1] */
+} dtmpc_adapt_cfg;
+
+/* Algorithm-2 closed-loop tube step configuration (core/tube_mpc.py:803-1023). */
+typedef struct dtmpc_tube_cfg {
+  dtmpc_cost nominal;       /* fixed nominal cost */
+  dtmpc_ilqr_cfg nom_ilqr;
+  dtmpc_ilqr_cfg aux_ilqr;
+  int32_t disturbance;      /* 0: w injected by the caller, 1: counter-based Philox on device */
+  int32_t write_log;        /* 1: write the per-step log record (see dtmpc_tube_state.log) */
+  uint64_t seed;            /* Philox key (disturbance == 1) */
+  double w_low[3];
+  double w_high[3];
+} dtmpc_tube_cfg;
+
+/* Device-resident closed-loop state; all SoA [fields][B] unless stated, caller-owned. */
+typedef struct dtmpc_tube_state {
+  void* x;          /* [3][B] plant state x_t */
+  void* b;          /* [B]    plant barrier state b_t */
+  void* xbar;       /* [3][B] nominal state */
+  void* bbar;       /* [B] */
+  void* Xnom;       /* [N+1][4][B] nominal optimal tape (written) */
+  void* Unom;       /* [N][2][B]  in: nominal warm start, out: shifted warm start */
+  void* Xaux;       /* [N+1][4][B] ancillary optimal tape (written) */
+  void* Uaux;       /* [N][2][B]  in: ancillary warm start, out: shifted warm start */
+  void* work;       /* dtmpc_tube_workspace_bytes() scratch */
+  const void* theta;/* [6] ancillary weights Qa(3), Ra(2), qba (shared by the batch) */
+  void* partials;   /* [nblocks][8] per-workgroup sums: L, gQ(3), gR(2), gqb, pad */
+  void* log;        /* [12][B] or NULL: x(3) u(2) xbar(3) ubar(2) b L of step t */
+  int32_t* status;  /* [B] DTMPC_ST_* bits (OR-accumulated) */
+  int32_t* iters;   /* [2][B] nominal / ancillary iterations used, or NULL */
+} dtmpc_tube_state;
+
+int dtmpc_abi_version(void);
+const char* dtmpc_last_error(void);
+
+/* Device count visible to the library (0 when no GPU). */
+int dtmpc_device_count(void);
+
+/* ---- KAT-level entry points (per-kernel parity) --------------------------------------- */
+
+/* rollout with f = DBaS-augmented Dubins step:
+ *   replaces core/ddp.py:89-99 `rollout` with f = f_hat_nom (core/tube_mpc.py:816-821),
+ *   i.e. core/barrier.py:75-108 `dbas_step` over core/systems/dubins.py:26-45 `dubins_step`.
+ *   x0 [4][B], U [N][2][B] (used as given, not clamped), X [N+1][4][B] out. */
+int dtmpc_dbas_rollout(int dtype, const dtmpc_spec* spec, int64_t B,
+                       const void* x0, const void* U, void* X, void* stream);
+
+/* b0 = B(h(x0)) for each trajectory: replaces core/barrier.py:111-120 `dbas_init_b0`.
+ *   x [3][B] (or the first 3 fields of any [F][B] array with F >= 3 via x), b [B] out. */
+int dtmpc_dbas_init(int dtype, const dtmpc_spec* spec, int64_t B, const void* x, void* b,
+                    void* stream);
+
+/* Per-step linearisation + cost derivatives along a tape:
+ *   replaces core/systems/dubins_aug_jac.py:61-139 `dubins_augmented_jacobian` and
+ *   core/cost_derivs.py:58-146 (`*_cost_derivs_u`, `*_terminal_derivs`).
+ *   A [N][16][B] (row-major 4x4), Bm [N][8][B] (row-major 4x2),
+ *   lx [N+1][4][B] (k = N is phi_x), lu [N][2][B].  Xref [N+1][3][B] / Uref [N][2][B] are read
+ *   only for DTMPC_COST_TRACK (may be NULL otherwise). */
+int dtmpc_linearize(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, int64_t B,
+                    const void* X, const void* U, const void* Xref, const void* Uref,
+                    void* A, void* Bm, void* lx, void* lu, void* stream);
+
+/* ---- solver entry points -------------------------------------------------------------- */
+
+/* Box-clamped iLQR with line search (all alphas, best-of, strict <) and per-trajectory tol exit:
+ *   replaces core/ddp.py:102-307 `ilqr_solve` for the typed problem.
+ *   x0 [4][B]; U [N][2][B] in: V_init (clamped first, core/ddp.py:127-129), out: V*;
+ *   X [N+1][4][B] out: X*; K [N][8][B] / kff [N][2][B] out: gains of the last backward pass
+ *   (may be NULL); iters [B] out (may be NULL); status [B] out (OR-accumulated). */
+int dtmpc_ilqr_solve(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
+                     const dtmpc_ilqr_cfg* cfg, int64_t B, const void* x0,
+                     const void* Xref, const void* Uref, void* X, void* U,
+                     void* K, void* kff, int32_t* iters, int32_t* status, void* stream);
+
+/* Scratch bytes for dtmpc_ddp_sensitivity. */
+size_t dtmpc_sensitivity_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t want_lambda);
+
+/* DDP-structured KKT sensitivity with active set (paper Appendix G):
+ *   replaces core/ddp.py:317-427 `ddp_sensitivity` driven by the paper-mode upper-loss closures
+ *   core/tube_mpc.py:924-957 (g_x = [2(x - xbar_k), 2 b], g_u = 0, terminal likewise).
+ *   X/U: ancillary optimum; Xbar [N+1][3][B]: nominal states of the upper loss;
+ *   Xref/Uref: ancillary cost references (DTMPC_COST_TRACK), cost: ancillary cost.
+ *   dX [N+1][4][B], dU [N][2][B], dlam [N+1][4][B] (NULL skips delta_lambda). */
+int dtmpc_ddp_sensitivity(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, int64_t B,
+                          const void* X, const void* U, const void* Xref, const void* Uref,
+                          const void* Xbar, void* dX, void* dU, void* dlam, void* work,
+                          int32_t* status, void* stream);
+
+/* Upper loss and analytic DOC gradient per trajectory:
+ *   replaces core/tube_mpc.py:915-919 (L) and :963-976 (gQ, gR, gqb).
+ *   out [7][B]: L, gQ(3), gR(2), gqb. */
+int dtmpc_doc_grad(int dtype, int32_t horizon, int64_t B, const void* Xaux, const void* Uaux,
+                   const void* Xnom, const void* Unom, const void* dX, const void* dU,
+                   void* out, void* stream);
+
+/* ---- fused closed-loop step (Algorithm 2 body) ----------------------------------------- */
+
+/* Scratch bytes for dtmpc_tube_step. */
+size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B);
+/* Number of per-workgroup partial records dtmpc_tube_step writes for a batch of B. */
+int64_t dtmpc_tube_partials_count(int64_t B);
+
+/* One closed-loop step for every trajectory (core/tube_mpc.py:803-1023 loop body):
+ *   nominal iLQR -> ancillary iLQR tracking it -> upper loss -> sensitivity -> DOC gradient
+ *   (per-workgroup sums into state->partials) -> plant step with disturbance -> nominal
+ *   propagation -> warm-start shift.  theta is READ (the update happens in
+ *   dtmpc_theta_update after the cross-rank sum).  w: [3][B] injected disturbance
+ *   (cfg->disturbance == 0) or NULL.  global_offset / step index key the Philox stream so that
+ *   every sharding of a global batch sees identical disturbances. */
+int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B,
+                    int64_t global_offset, int64_t step, const dtmpc_tube_state* state,
+                    const void* w, void* stream);
+
+/* Fixed-order sum of the per-workgroup partial records: sums [8] (L, gQ(3), gR(2), gqb, 0). */
+int dtmpc_partials_reduce(int dtype, int64_t n_partials, const void* partials, void* sums,
+                          void* stream);
+
+/* Momentum + projected update of the shared ancillary weights (core/tube_mpc.py:978-984) with
+ * the batch-mean gradient g = sums[1:7] * inv_batch.  theta [6] and velocity [6] in/out. */
+int dtmpc_theta_update(int dtype, const dtmpc_adapt_cfg* cfg, double inv_batch, const void* sums,
+                       void* theta, void* velocity, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DTMPC_H */
