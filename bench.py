@@ -1,0 +1,214 @@
+"""Benchmark: DDP+IFT iterations/s of the batched Dubins+DBaS tube-MPC closed-loop step (T = 50).
+
+One bench "step" = one Algorithm-2 closed-loop step for every trajectory (core/tube_mpc.py:803-1023):
+nominal iLQR (10 fixed iterations, 7 line-search alphas) + ancillary iLQR (20 fixed iterations) + one
+IFT pass (DDP sensitivity + DOC gradient) + cross-rank gradient all-reduce + theta update + plant step.
+metric value = trajectories_all_ranks * (10 + 20 + 1) / seconds_per_step   
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_per_gpu] [--no-cpu]
+        (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "differentiable-tube-mpc_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from diff_tube_mpc_strict_pt.core import TubeMPC, shard_range  # noqa: E402
+from diff_tube_mpc_strict_pt.core.problem import paper_config, paper_setup_from_config  # noqa: E402
+
+# SURVEY.md §8d algorithmic HBM bytes per trajectory per closed-loop step (phase-split tape traffic):
+# 10 nominal iterations x 7,652 B + 20 ancillary iterations x 9,676 B + one IFT pass 4,284 B.
+ALGO_BYTES_PER_TRAJ_STEP = 10 * 7652 + 20 * 9676 + 4284  # = 274,324
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+ITERS_PER_STEP = 10 + 20 + 1
+
+
+def bench_setup(dtype_name: str):
+    cfg = paper_config()
+    st = paper_setup_from_config(cfg)
+    # benchmark mode: fixed iteration counts (tol = -1, no early exit), SURVEY.md §8d
+    import dataclasses
+
+    nom = dataclasses.replace(st.ilqr_nom, tol=-1.0)
+    aux = dataclasses.replace(st.ilqr_aux, tol=-1.0)
+    return dataclasses.replace(st, ilqr_nom=nom, ilqr_aux=aux)
+
+
+def initial_states(lo: int, hi: int, device, dtype) -> torch.Tensor:
+    """x0 per GLOBAL trajectory index: px, py ~ U[0,1], theta ~ U[0, pi/2]; generated
+    in global order so every sharding sees the same inputs."""
+    g = torch.Generator().manual_seed(0)
+    n = hi
+    u = torch.rand(n, 3, generator=g, dtype=torch.float64)[lo:hi]
+    x0 = torch.stack([u[:, 0], u[:, 1], u[:, 2] * (np.pi / 2)], 1)
+    return x0.to(device=device, dtype=dtype)
+
+
+def pmc_traffic(batch: int):
+    """Per-launch HBM bytes of tube_step_kernel from a committed rocprofv3 --pmc summary (or None).
+    FETCH_SIZE is doubled (gfx950 under-reports wide coalesced reads by 2x, MI355X_MICROARCH.md §HBM)."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if int(d.get("batch", -1)) == batch and "tube_step_bytes_per_launch" in d:
+            best = float(d["tube_step_bytes_per_launch"])
+    return best
+
+
+def cpu_baseline(setup, seconds_target: float = 15.0):
+    """The C oracle (oracle/liboracle.so, a restatement of the reference) timed on host cores."""
+    from diff_tube_mpc_strict_pt import _abi
+    from oracle.oracle import Oracle, build
+
+    build()
+    threads = int(os.environ.get("DTMPC_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    o = Oracle(np.float32, nthreads=threads)
+    N = setup.problem.horizon
+    sp = setup.problem.to_c()
+    tcfg = _abi.DtmpcTubeCfg()
+    tcfg.nominal = setup.nominal_cost.to_c()
+    tcfg.nom_ilqr = setup.ilqr_nom.to_c()
+    tcfg.aux_ilqr = setup.ilqr_aux.to_c()
+    tcfg.disturbance = 1
+    for f in range(3):
+        tcfg.w_low[f], tcfg.w_high[f] = setup.w_low[f], setup.w_high[f]
+
+    def run(B):
+        x0 = initial_states(0, B, "cpu", torch.float32).numpy().T.copy()
+        h, _, _ = o.h_eval(sp, x0[0], x0[1])
+        b0 = o.barrier(sp, h)[0]
+        state = {"x": x0, "b": b0.copy(), "xbar": x0.copy(), "bbar": b0.copy(),
+                 "Xnom": np.zeros((N + 1, 4, B), np.float32), "Unom": np.zeros((N, 2, B), np.float32),
+                 "Xaux": np.zeros((N + 1, 4, B), np.float32), "Uaux": np.zeros((N, 2, B), np.float32)}
+        t0 = time.perf_counter()
+        o.tube_step(sp, tcfg, state, np.array(setup.theta0, np.float32), step=0, want_log=False)
+        return time.perf_counter() - t0
+
+    B = 4 * threads
+    dt = run(B)
+    B = int(min(262144, max(B, B * seconds_target / max(dt, 1e-3))))
+    B -= B % threads
+    dt = run(B)
+    return {"value": B * ITERS_PER_STEP / dt, "unit": "DDP+IFT iters/s", "cores": threads, "kind": "port",
+            "sample": f"C oracle (oracle/dtmpc_oracle.c) f32, one closed-loop step of {B} trajectories "
+                      f"(10+20 fixed iLQR iterations, 7 alphas, + IFT), OpenMP {threads} threads, {dt:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=65536, help="trajectories per GPU (weak scaling)")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    dtype = torch.float32 if args.dtype == "f32" else torch.float64
+    setup = bench_setup(args.dtype)
+    Bg = args.batch * world
+    lo, hi = shard_range(Bg, rank, world)
+    mpc = TubeMPC(setup, batch=hi - lo, device=dev, dtype=dtype, disturbance="philox", seed=0,
+                  global_offset=lo, global_batch=Bg, process_group=group)
+    mpc.reset(initial_states(lo, hi, dev, dtype))
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        mpc.step()
+    barrier()
+    # HIP events on the launch stream: whole step, and the fused tube_step kernel alone
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        e0, e1 = ev[s]
+        e0.record()
+        mpc.step(kernel_events=kev[s])
+        e1.record()
+    barrier()
+    wall = time.perf_counter() - t0
+    step_ms = [e0.elapsed_time(e1) for e0, e1 in ev]
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in kev]))
+    mpc.check()
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+    wall = float(wall_t)
+
+    ms_per_step = 1e3 * wall / args.steps
+    value = Bg * ITERS_PER_STEP / (wall / args.steps)
+    algo_bytes = ALGO_BYTES_PER_TRAJ_STEP * (hi - lo)
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(hi - lo)
+    out = {
+        "metric": "DDP+IFT iters/sec, batched Dubins+DBaS T=50",
+        "value": value,
+        "unit": "DDP+IFT iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic: x0 ~ U[0,1]^2 x U[0,pi/2] per global index, Philox disturbances, configs/dubins.yaml values",
+        "config": {
+            "workload": "Algorithm-2 tube step: nominal iLQR 10 it + ancillary iLQR 20 it (7 alphas, tol=-1) + IFT",
+            "global_batch": Bg, "batch_per_gpu": hi - lo, "horizon": setup.problem.horizon, "obstacles": 5,
+            "line_search_alphas": len(setup.ilqr_nom.line_search_alphas), "parallelism": f"dp{world}",
+        },
+        "kernel_ms": kern_ms,
+        "event_ms_per_step_median": float(np.median(step_ms)),
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algo_bytes_per_launch": algo_bytes,
+        },
+    }
+    if rank == 0 and not args.no_cpu and world == 1:
+        out["cpu_baseline"] = cpu_baseline(setup)
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

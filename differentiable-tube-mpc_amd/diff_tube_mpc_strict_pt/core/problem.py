@@ -237,6 +237,35 @@ def paper_setup_from_config(cfg: Dict[str, Any]) -> PaperSetup:
     )
 
 
+def paper_config() -> Dict[str, Any]:
+    """The experiment configuration of the reference (values of configs/dubins.yaml:1-85), as a dict
+    in the same schema run_closed_loop_experiment reads (core/tube_mpc.py:48-181, 674-768)."""
+    return {
+        "seed": 0,
+        "device": "cuda",
+        "use_float64": True,
+        "paper_dubins_mode": True,
+        "system": {
+            "name": "dubins", "dt": 0.01, "horizon_N": 50, "task_horizon_H": 300,
+            "nominal_max_iter": 10, "aux_max_iter": 20, "ilqr_reg": 1.0e-3,
+            "line_search_alphas": [1.0, 0.5, 0.25, 0.1, 0.05, 0.01, 0.0],
+            "control_bounds": {"v_min": -10.0, "v_max": 10.0, "omega_max": math.pi},
+            "disturbance": {"w_low": [-0.05, -0.05, -0.05], "w_high": [0.05, 0.05, 0.05]},
+            "target": [10.0, 10.0, math.pi / 4],
+        },
+        "dbas": {"barrier_type": "inverse", "alpha": 0.0, "gamma": 0.0, "nominal_tightening": 0.0, "eps": 1.0e-4},
+        "environment": {
+            "obstacles": [{"center": c, "radius": 1.0} for c in ([4.0, 2.0], [2.0, 4.0], [4.0, 8.0], [8.0, 4.0], [6.0, 6.0])],
+            "obstacle_smoothmin_beta": 20.0,
+            "obstacle_aggregation": "smoothmin",
+        },
+        "cost_nominal": {"Q": [1.0, 1.0, 0.0], "R": [1.0, 1.0], "q_b": 1.0, "Qf": [1000.0, 1000.0, 1000.0]},
+        "cost_auxiliary": {"Q": [1.0, 1.0, 1.0], "R": [1.0, 1.0], "q_b": 1.0},
+        "adaptation": {"lr_eta": 5.0e-2, "steps": 1, "momentum": 0.9, "adapt_nominal": False,
+                       "adapt_ancillary": True, "project_params": True},
+    }
+
+
 def tracking_cost(theta: Sequence[float]) -> QuadraticCost:
     """Ancillary tracking cost with weights theta = (Qa, Ra, qba); terminal weight Qa
     (core/tube_mpc.py:875-894)."""

@@ -171,8 +171,9 @@ class TubeMPC:
     def _stream(self) -> int:
         return int(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def step(self, w: Optional[Tensor] = None) -> None:
-        """One closed-loop step for the whole batch (asynchronous on the current stream)."""
+    def step(self, w: Optional[Tensor] = None, kernel_events=None) -> None:
+        """One closed-loop step for the whole batch (asynchronous on the current stream).
+        kernel_events: optional (start, end) torch.cuda.Event pair recorded around the fused kernel."""
         wp = None
         if self.cfg.disturbance == 0:
             if w is None or w.shape != (self.B, 3):
@@ -180,9 +181,13 @@ class TubeMPC:
             self._w = w.to(device=self.device, dtype=self.dtype).t().contiguous()
             wp = self._w.data_ptr()
         s = self._stream()
+        if kernel_events is not None:
+            kernel_events[0].record()
         _lib.check(self.lib.dtmpc_tube_step(self._dt, C.byref(self.spec), C.byref(self.cfg), self.B,
                                             self.global_offset, self.t, C.byref(self.state), wp, s),
                    "dtmpc_tube_step")
+        if kernel_events is not None:
+            kernel_events[1].record()
         _lib.check(self.lib.dtmpc_partials_reduce(self._dt, self.n_partials, self.partials.data_ptr(),
                                                   self.sums.data_ptr(), s), "dtmpc_partials_reduce")
         allreduce_sums(self.sums, self.group)
