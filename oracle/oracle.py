@@ -18,6 +18,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB_PATHS = {"plain": LIB_PATH, "fma": os.path.join(HERE, "liboracle_fma.so")}
 _REPO = os.path.dirname(HERE)
 _PKG_ROOT = os.path.join(_REPO, "differentiable-tube-mpc_amd")
 if _PKG_ROOT not in sys.path:
@@ -25,24 +26,25 @@ if _PKG_ROOT not in sys.path:
 
 from diff_tube_mpc_strict_pt import _abi  # noqa: E402  (plain ctypes structs, no compute)
 
-_lib = None
+_libs: dict = {}
 
 
 def build(force: bool = False) -> str:
     srcs = [os.path.join(HERE, f) for f in ("dtmpc_oracle.c", "oracle_impl.h", "Makefile")]
     srcs.append(os.path.join(_REPO, "include", "dtmpc.h"))
-    if force or not os.path.exists(LIB_PATH) or any(os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in srcs):
-        subprocess.run(["make", "-B", "-C", HERE, "liboracle.so"], check=True, stdout=subprocess.DEVNULL)
+    stale = force or any(
+        not os.path.exists(p) or any(os.path.getmtime(s) > os.path.getmtime(p) for s in srcs) for p in LIB_PATHS.values())
+    if stale:
+        subprocess.run(["make", "-B", "-C", HERE, "all"], check=True, stdout=subprocess.DEVNULL)
     return LIB_PATH
 
 
-def load() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def load(variant: str = "plain") -> C.CDLL:
+    if variant not in _libs:
+        if not os.path.exists(LIB_PATHS[variant]):
             build()
-        _lib = C.CDLL(LIB_PATH)
-    return _lib
+        _libs[variant] = C.CDLL(LIB_PATHS[variant])
+    return _libs[variant]
 
 
 def _p(a):
@@ -60,13 +62,13 @@ def aos(a: np.ndarray) -> np.ndarray:
 
 
 class Oracle:
-    def __init__(self, dtype=np.float64, nthreads: int = 1):
+    def __init__(self, dtype=np.float64, nthreads: int = 1, variant: str = "plain"):
         self.dt = np.dtype(dtype)
         if self.dt not in (np.dtype(np.float64), np.dtype(np.float32)):
             raise ValueError("float32 or float64")
         self.sfx = "_f64" if self.dt == np.float64 else "_f32"
         self.nthreads = int(nthreads)
-        self.lib = load()
+        self.lib = load(variant)
 
     def _f(self, name):
         return getattr(self.lib, name + self.sfx)

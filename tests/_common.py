@@ -44,6 +44,23 @@ def rel(a, b) -> float:
     return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
 
 
+def rel_rows(a, b) -> np.ndarray:
+    """rel() per trajectory (leading axis)."""
+    return np.array([rel(a[i], b[i]) for i in range(len(a))])
+
+
+def agreement(dev_out, plain, fma, base: float, k: float = 10.0):
+    """Per-trajectory agreement of a device result with the oracle.
+
+    Two valid IEEE evaluation orders of the same algorithm -- the oracle built without (plain) and with
+    fused multiply-add contraction (fma) -- already differ by s_i on trajectory i (line-search near-ties,
+    tol-exit knife edges, barrier-dominated ill-conditioning).  The device result is accepted when it is
+    within max(base, k * s_i) of either build.  Returns (fraction ok, per-trajectory errors, spreads)."""
+    e = np.minimum(rel_rows(dev_out, plain), rel_rows(dev_out, fma))
+    s = rel_rows(plain, fma)
+    return float(np.mean(e <= np.maximum(base, k * s))), e, s
+
+
 def tol_for(dtype, cond: float) -> float:
     """Comparison tolerance from the reference's own conditioning on that case."""
     base = 1e-9 if np.dtype(dtype) == np.float64 else 1e-3
