@@ -6,7 +6,9 @@
  * leg, and by nothing else.  The algorithm is restated in oracle_impl.h; each function there cites
  * the reference file:line it follows.
  */
+#include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "../include/dtmpc.h"
 
@@ -42,13 +44,58 @@ void oracle_philox_bits(uint64_t seed, uint64_t gidx, uint64_t step, uint32_t* o
 
 int oracle_abi_version(void) { return DTMPC_ABI_VERSION; }
 
+#ifdef ORACLE_ULP_NOISE
+/* Calibration build (liboracle_ulp.so): every transcendental result is moved by one ulp up or down,
+ * chosen by a hash of the argument's bits.  The spread between this build and liboracle.so measures
+ * how sensitive a case is to last-bit differences between math libraries (glibc vs the GPU's). */
+static uint64_t ulp_hash(uint64_t v) {
+  v ^= v >> 33;
+  v *= 0xff51afd7ed558ccdULL;
+  v ^= v >> 33;
+  v *= 0xc4ceb9fe1a85ec53ULL;
+  v ^= v >> 33;
+  return v;
+}
+static double ulpn_d(double v, double x) {
+  uint64_t b;
+  memcpy(&b, &x, sizeof b);
+  return nextafter(v, (ulp_hash(b) & 1) ? INFINITY : -INFINITY);
+}
+static float ulpn_f(float v, float x) {
+  uint32_t b;
+  memcpy(&b, &x, sizeof b);
+  return nextafterf(v, (ulp_hash(b) & 1) ? INFINITY : -INFINITY);
+}
+#define D_EXP(x) ulpn_d(exp(x), (x))
+#define D_LOG(x) ulpn_d(log(x), (x))
+#define D_SIN(x) ulpn_d(sin(x), (x))
+#define D_COS(x) ulpn_d(cos(x), (x) + 1.0)
+#define D_ATAN2(y, x) ulpn_d(atan2((y), (x)), (y))
+#define F_EXP(x) ulpn_f(expf(x), (x))
+#define F_LOG(x) ulpn_f(logf(x), (x))
+#define F_SIN(x) ulpn_f(sinf(x), (x))
+#define F_COS(x) ulpn_f(cosf(x), (x) + 1.0f)
+#define F_ATAN2(y, x) ulpn_f(atan2f((y), (x)), (y))
+#else
+#define D_EXP exp
+#define D_LOG log
+#define D_SIN sin
+#define D_COS cos
+#define D_ATAN2 atan2
+#define F_EXP expf
+#define F_LOG logf
+#define F_SIN sinf
+#define F_COS cosf
+#define F_ATAN2 atan2f
+#endif
+
 #define REAL double
 #define SUFFIX _f64
-#define M_EXP exp
-#define M_LOG log
-#define M_SIN sin
-#define M_COS cos
-#define M_ATAN2 atan2
+#define M_EXP D_EXP
+#define M_LOG D_LOG
+#define M_SIN D_SIN
+#define M_COS D_COS
+#define M_ATAN2 D_ATAN2
 #define M_FABS fabs
 #include "oracle_impl.h"
 #undef REAL
@@ -62,10 +109,10 @@ int oracle_abi_version(void) { return DTMPC_ABI_VERSION; }
 
 #define REAL float
 #define SUFFIX _f32
-#define M_EXP expf
-#define M_LOG logf
-#define M_SIN sinf
-#define M_COS cosf
-#define M_ATAN2 atan2f
+#define M_EXP F_EXP
+#define M_LOG F_LOG
+#define M_SIN F_SIN
+#define M_COS F_COS
+#define M_ATAN2 F_ATAN2
 #define M_FABS fabsf
 #include "oracle_impl.h"

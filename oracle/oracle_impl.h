@@ -1026,7 +1026,8 @@ void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long 
       st |= FN(sens1)(&s, &ca, Xa, Va, Xr, Vn, Xr, dXa, dVa, NULL, wk2);
       REAL o[7];
       FN(docgrad1)(N, Xa, Va, Xn, Vn, dXa, dVa, o);
-      for (int j = 0; j < 7; ++j) gout[(long long)j * B + i] = o[j];
+      /* a flagged (non-finite) trajectory contributes nothing to the shared gradient */
+      for (int j = 0; j < 7; ++j) gout[(long long)j * B + i] = st ? (REAL)0 : o[j];
       /* plant + nominal propagation :990-1001 */
       REAL u[2] = {Va[0], Va[1]}, ub[2] = {Vn[0], Vn[1]};
       REAL ww[3];

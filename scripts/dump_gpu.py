@@ -32,16 +32,32 @@ def main():
     x0 = np.concatenate([x, b[:, None]], 1)
     V0 = np.stack([rng.uniform(-1, 3, (B, N)), rng.uniform(-1, 1, (B, N))], 2)
     out = {"x0": x0, "V0": V0}
-    for tag, dt in (("f64", torch.float64), ("f32", torch.float32)):
-        for mi in range(1, 6):
+    for tag, dt in (("f64", torch.float64),):
+        for mi in (5,):
             r = ilqr_solve(problem=st.problem, cost=st.nominal_cost, cfg=ilqr_cfg(mi, -1.0),
                            x0=torch.as_tensor(x0, dtype=dt, device=dev), V_init=torch.as_tensor(V0, dtype=dt, device=dev),
                            check=False)
             out[f"X_{tag}_{mi}"] = r.X.cpu().numpy()
             out[f"V_{tag}_{mi}"] = r.V.cpu().numpy()
-            out[f"K_{tag}_{mi}"] = r.K.cpu().numpy()
-            out[f"k_{tag}_{mi}"] = r.k.cpu().numpy()
             out[f"st_{tag}_{mi}"] = r.status.cpu().numpy()
+    # tracking solves of the oracle's nominal plans (as in test_ilqr_batched_vs_oracle)
+    from diff_tube_mpc_strict_pt.core import tracking_cost
+
+    Xp, Vp, _, _, _, _ = o.ilqr_solve(sp, st.nominal_cost.to_c(), ilqr_cfg(10, 1e-3).to_c(), x0, V0)
+    cost = tracking_cost((0.7, 1.3, 0.2, 0.5, 2.0, 0.8))
+    xa = x0.copy()
+    xa[:, :2] += 0.02
+    Va0 = np.roll(Vp, -1, axis=1)
+    out.update(Xp=Xp, Vp=Vp, xa=xa, Va0=Va0)
+    for mi in range(1, 7):
+        r = ilqr_solve(problem=st.problem, cost=cost, cfg=ilqr_cfg(mi, -1.0),
+                       x0=torch.as_tensor(xa, dtype=torch.float64, device=dev),
+                       V_init=torch.as_tensor(Va0, dtype=torch.float64, device=dev),
+                       X_ref=torch.as_tensor(Xp, dtype=torch.float64, device=dev),
+                       U_ref=torch.as_tensor(Vp, dtype=torch.float64, device=dev), check=False)
+        out[f"Xa_{mi}"] = r.X.cpu().numpy()
+        if mi == 6:
+            out[f"Ka_{mi}"] = r.K.cpu().numpy()
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     np.savez_compressed(os.path.join(REPO, "gpurun_out", "dump_ilqr.npz"), **out)
     print("dumped")
