@@ -5,6 +5,12 @@ nominal iLQR (10 fixed iterations, 7 line-search alphas) + ancillary iLQR (20 fi
 IFT pass (DDP sensitivity + DOC gradient) + cross-rank gradient all-reduce + theta update + plant step.
 metric value = trajectories_all_ranks * (10 + 20 + 1) / seconds_per_step   
 
+Every timed step is the first closed-loop step of a fresh episode over the same synthetic batch
+(reset: x0, b0 = B(h(x0)), zero warm starts, theta0 -- inside the timed region).  Free-running the loop
+instead is not a stable workload in f32: from step 1 on, a few trajectories' ancillary plans enter an
+obstacle (b ~ 1e10, also in f64), their f32 IFT gradients are ill-conditioned (|g| ~ 1e15-1e30), the
+batch-mean theta jumps to ~1e10 and trajectories start to overflow.
+
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_per_gpu] [--no-cpu]
         (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 """
@@ -137,7 +143,11 @@ def main() -> None:
     lo, hi = shard_range(Bg, rank, world)
     mpc = TubeMPC(setup, batch=hi - lo, device=dev, dtype=dtype, disturbance="philox", seed=0,
                   global_offset=lo, global_batch=Bg, process_group=group)
-    mpc.reset(initial_states(lo, hi, dev, dtype))
+    x0 = initial_states(lo, hi, dev, dtype)
+
+    def step(kernel_events=None):
+        mpc.reset(x0)
+        mpc.step(kernel_events=kernel_events)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -146,7 +156,7 @@ def main() -> None:
             torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
-        mpc.step()
+        step()
     barrier()
     # HIP events on the launch stream: whole step, and the fused tube_step kernel alone
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -155,14 +165,14 @@ def main() -> None:
     for s in range(args.steps):
         e0, e1 = ev[s]
         e0.record()
-        mpc.step(kernel_events=kev[s])
+        step(kernel_events=kev[s])
         e1.record()
     barrier()
     wall = time.perf_counter() - t0
     step_ms = [e0.elapsed_time(e1) for e0, e1 in ev]
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in kev]))
     # f32 can overflow on trajectories driven deep into an obstacle's relaxed barrier, exactly where the
-    # reference raises FloatingPointError in f32; such trajectories are flagged and frozen, and counted.
+    # reference raises FloatingPointError in f32; such trajectories are flagged and counted (last step).
     flagged = torch.tensor([int((mpc.status != 0).sum())], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(flagged)
@@ -190,7 +200,8 @@ def main() -> None:
         "dtype": args.dtype,
         "data": "synthetic: x0 ~ U[0,1]^2 x U[0,pi/2] per global index, Philox disturbances, configs/dubins.yaml values",
         "config": {
-            "workload": "Algorithm-2 tube step: nominal iLQR 10 it + ancillary iLQR 20 it (7 alphas, tol=-1) + IFT",
+            "workload": "Algorithm-2 tube step (episode start): nominal iLQR 10 it + ancillary iLQR 20 it "
+                        "(7 alphas, tol=-1) + IFT + theta all-reduce/update + plant",
             "global_batch": Bg, "batch_per_gpu": hi - lo, "horizon": setup.problem.horizon, "obstacles": 5,
             "line_search_alphas": len(setup.ilqr_nom.line_search_alphas), "parallelism": f"dp{world}",
         },

@@ -26,15 +26,26 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in [SRC, *DEPS, __file__])
 
 
-def build(force: bool = False) -> str:
-    if not force and up_to_date():
-        return OUT
-    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", SRC]
+def build(force: bool = False, variant: str = "", defines=()) -> str:
+    """Build the library.  ``variant`` (with extra ``-D`` defines) writes libdtmpc_<variant>.so next to
+    the product library, for A/B kernel experiments loaded through DTMPC_LIBRARY; it never replaces
+    libdtmpc.so."""
+    out = OUT if not variant else OUT.replace("libdtmpc.so", f"libdtmpc_{variant}.so")
+    if not variant and not force and up_to_date():
+        return out
+    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-o", out + ".tmp", SRC]
     print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--variant", default="")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    print(build(force=a.force, variant=a.variant, defines=a.defines))

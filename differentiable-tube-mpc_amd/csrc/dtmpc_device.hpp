@@ -18,13 +18,20 @@
 namespace dtmpc {
 
 // ---------------------------------------------------------------------------------------------
-// math helpers (precision-overloaded)
+// math helpers (precision-overloaded).
+// f64 (parity builds) uses the OCML functions.  f32 (the benchmark precision) uses the CDNA4
+// transcendental units directly for exp / log (v_exp_f32 / v_log_f32, base 2) and reciprocals
+// (v_rcp_f32): 1-2 instructions each instead of 15-40.  sin/cos stay on OCML sincosf: the native
+// v_sin_f32 / v_cos_f32 were measured (round 1) to push the f32 tube-step gradients and nominal
+// plans outside the oracle-calibrated parity gates of tests/test_gpu_parity.py, for a 9 % gain.
 __device__ __forceinline__ void m_sincos(float x, float* s, float* c) { sincosf(x, s, c); }
 __device__ __forceinline__ void m_sincos(double x, double* s, double* c) { sincos(x, s, c); }
-__device__ __forceinline__ float m_exp(float x) { return expf(x); }
+__device__ __forceinline__ float m_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
 __device__ __forceinline__ double m_exp(double x) { return exp(x); }
-__device__ __forceinline__ float m_log(float x) { return logf(x); }
+__device__ __forceinline__ float m_log(float x) { return __builtin_amdgcn_logf(x) * 0.693147180559945309f; }
 __device__ __forceinline__ double m_log(double x) { return log(x); }
+__device__ __forceinline__ float m_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ double m_rcp(double x) { return 1.0 / x; }
 __device__ __forceinline__ float m_atan2(float y, float x) { return atan2f(y, x); }
 __device__ __forceinline__ double m_atan2(double y, double x) { return atan2(y, x); }
 __device__ __forceinline__ float m_abs(float x) { return fabsf(x); }
@@ -69,12 +76,17 @@ struct DIlqr {
   T alphas[DTMPC_MAX_ALPHAS];
 };
 
-// Per-thread strided view of one trajectory inside a SoA [rows][F][B] array.
+// One trajectory's view of a SoA [rows][F][B] array: element (k, f) of lane `lane` lives at
+// base[(k*F + f)*ld + lane].  base/ld/k are wave-uniform, so the plane address is scalar (SALU) and
+// the per-lane part is a single 32-bit offset: one coalesced 256 B (f32) line per wave per access.
 template <typename T>
 struct Col {
-  T* p;
-  int ld;  // B
-  __device__ __forceinline__ T& at(int k, int F, int f) const { return p[(k * F + f) * ld]; }
+  T* base;
+  unsigned ld;    // B
+  unsigned lane;  // trajectory index
+  __device__ __forceinline__ T& at(int k, int F, int f) const {
+    return (base + (size_t)((unsigned)(k * F + f) * ld))[lane];
+  }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -91,6 +103,10 @@ __device__ __forceinline__ T h_circle(const DSpec<T>& s, int i, T px, T py) {  /
 //   smoothmin: h_multi_circle_obstacles :41-69 (stable LSE, two passes)
 //   min:       h_min_circle_obstacles :95-106
 //   single:    h_circle_obstacle :16-30;  none: 1 (run_nominal.py:256)
+// The W-wide value path stays two-pass: holding all z_i for W points in registers (tried, round 1)
+// pushed the fused tube kernel into AGPR spills and scratch.  h_grad (W = 1) keeps z_i in registers.
+constexpr int kFastObs = 8;
+
 template <typename T, int W>
 __device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* py, T* h) {
   if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0) {
@@ -137,6 +153,30 @@ __device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* p
 // e_i * (1/sum e) instead of e_i / sum e (one reciprocal per point).
 template <typename T>
 __device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy) {
+  if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0 && s.M <= kFastObs) {
+    T z[kFastObs], zmax = T(0);
+#pragma unroll
+    for (int i = 0; i < kFastObs; ++i) {
+      if (i < s.M) {
+        z[i] = s.neg_beta * h_circle(s, i, px, py);
+        zmax = (i == 0 || z[i] > zmax) ? z[i] : zmax;
+      }
+    }
+    T se = T(0), sx = T(0), sy = T(0);
+#pragma unroll
+    for (int i = 0; i < kFastObs; ++i) {
+      if (i < s.M) {
+        T e = m_exp(z[i] - zmax);
+        se += e;
+        sx += e * (T(2) * (px - s.cx[i]));
+        sy += e * (T(2) * (py - s.cy[i]));
+      }
+    }
+    T inv = m_rcp(se);
+    gx = sx * inv;
+    gy = sy * inv;
+    return s.neg_inv_beta * (zmax + m_log(se));
+  }
   if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0) {
     T zmax = s.neg_beta * h_circle(s, 0, px, py);
     for (int i = 1; i < s.M; ++i) {
@@ -150,7 +190,7 @@ __device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy)
       sx += e * (T(2) * (px - s.cx[i]));
       sy += e * (T(2) * (py - s.cy[i]));
     }
-    T inv = T(1) / se;
+    T inv = m_rcp(se);
     gx = sx * inv;
     gy = sy * inv;
     return s.neg_inv_beta * (zmax + m_log(se));
@@ -188,7 +228,7 @@ __device__ __forceinline__ T barrier_relaxed(const DSpec<T>& s, T z) {
   T a = s.alpha > s.eps ? s.alpha : s.eps;
   if (z >= a) {
     T zc = z < s.eps ? s.eps : z;
-    return T(1) / zc;
+    return m_rcp(zc);
   }
   T diff = z - a;
   T a2 = a * a;
@@ -201,7 +241,7 @@ __device__ __forceinline__ T dbarrier_relaxed(const DSpec<T>& s, T z) {
   T a = s.alpha > s.eps ? s.alpha : s.eps;
   if (z >= a) {
     T zc = z < s.eps ? s.eps : z;
-    return T(-1) / (zc * zc);
+    return -m_rcp(zc * zc);
   }
   T diff = z - a;
   T a2 = a * a;
@@ -360,10 +400,10 @@ __device__ __forceinline__ LU2<T> lu2(T m00, T m01, T m10, T m11) {
   f.sw = m_abs(m10) > m_abs(m00);
   T a00 = f.sw ? m10 : m00, a01 = f.sw ? m11 : m01;
   T a10 = f.sw ? m00 : m10, a11 = f.sw ? m01 : m11;
-  f.inv00 = T(1) / a00;
+  f.inv00 = m_rcp(a00);
   f.l = a10 * f.inv00;
   T u11 = a11 - f.l * a01;
-  f.inv11 = T(1) / u11;
+  f.inv11 = m_rcp(u11);
   f.a00 = a00;
   f.a01 = a01;
   return f;

@@ -78,8 +78,9 @@ static DIlqr<T> make_ilqr(const dtmpc_ilqr_cfg& c) {
 template <typename T>
 __device__ __forceinline__ Col<T> col(void* p, int64_t i, int B) {
   Col<T> c;
-  c.p = p ? reinterpret_cast<T*>(p) + i : nullptr;
-  c.ld = B;
+  c.base = reinterpret_cast<T*>(p);
+  c.ld = (unsigned)B;
+  c.lane = (unsigned)i;
   return c;
 }
 template <typename T>
@@ -342,7 +343,8 @@ __global__ void __launch_bounds__(kBlock) tube_step_kernel(DSpec<T> s, DCost<T> 
       lg[8 * nb + i] = v0;
       lg[9 * nb + i] = v1;
       lg[10 * nb + i] = xb;
-      lg[11 * nb + i] = acc[0];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) lg[(11 + j) * nb + i] = acc[j];
     }
     {
       T p0[1] = {x0}, p1[1] = {x1}, p2[1] = {x2}, pb[1] = {xb}, q0[1] = {u0}, q1[1] = {u1};

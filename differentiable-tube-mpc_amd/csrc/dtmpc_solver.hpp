@@ -74,12 +74,26 @@ __device__ bool ilqr_backward(const DSpec<T>& s, const DCost<T>& c, T reg, const
   T hn = h_grad(s, xn0, xn1, gxn, gyn);
   T dBn = dbarrier_relaxed(s, hn);
   bool ok = finite(R.Vx[0]) && finite(R.Vx[1]) && finite(R.Vx[2]) && finite(R.Vx[3]);
+  // prefetched step inputs (x_k, u_k, references), one step ahead of the recursion
+  T p0 = X.at(N - 1, 4, 0), p1 = X.at(N - 1, 4, 1), p2 = X.at(N - 1, 4, 2), pb = X.at(N - 1, 4, 3);
+  T pu0 = U.at(N - 1, 2, 0), pu1 = U.at(N - 1, 2, 1), pr0, pr1, pr2, pq0, pq1;
+  load_ref(c, Xr, rf, N - 1, pr0, pr1, pr2);
+  load_uref(c, Ur, N - 1, pq0, pq1);
   for (int k = N - 1; k >= 0; --k) {
-    T x0 = X.at(k, 4, 0), x1 = X.at(k, 4, 1), x2 = X.at(k, 4, 2), xb = X.at(k, 4, 3);
-    T u0 = U.at(k, 2, 0), u1 = U.at(k, 2, 1);
-    T q0, q1;
-    load_ref(c, Xr, rf, k, r0, r1, r2);
-    load_uref(c, Ur, k, q0, q1);
+    T x0 = p0, x1 = p1, x2 = p2, xb = pb, u0 = pu0, u1 = pu1, q0 = pq0, q1 = pq1;
+    r0 = pr0;
+    r1 = pr1;
+    r2 = pr2;
+    if (k > 0) {
+      p0 = X.at(k - 1, 4, 0);
+      p1 = X.at(k - 1, 4, 1);
+      p2 = X.at(k - 1, 4, 2);
+      pb = X.at(k - 1, 4, 3);
+      pu0 = U.at(k - 1, 2, 0);
+      pu1 = U.at(k - 1, 2, 1);
+      load_ref(c, Xr, rf, k - 1, pr0, pr1, pr2);
+      load_uref(c, Ur, k - 1, pq0, pq1);
+    }
     T sn, cs;
     m_sincos(x2, &sn, &cs);
     T gxk, gyk;
@@ -112,6 +126,33 @@ __device__ bool ilqr_backward(const DSpec<T>& s, const DCost<T>& c, T reg, const
 }
 
 // ---------------------------------------------------------------------------------------------
+// Everything the forward passes read at step k: old tape X[k], V[k], gains K[k], k[k] and the
+// tracking references.  Loaded one step ahead (software prefetch): with one wave per SIMD at the
+// benchmark batch there is no other wave to hide HBM latency behind.
+template <typename T>
+struct StepIn {
+  T X0, X1, X2, X3, V0, V1, K[8], k0, k1, r0, r1, r2, q0, q1;
+};
+
+template <typename T>
+__device__ __forceinline__ void load_step(StepIn<T>& L, const DCost<T>& c, const Col<T>& X,
+                                          const Col<T>& U, const Col<T>& K, const Col<T>& kf,
+                                          const Col<T>& Xr, int rf, const Col<T>& Ur, int k) {
+  L.X0 = X.at(k, 4, 0);
+  L.X1 = X.at(k, 4, 1);
+  L.X2 = X.at(k, 4, 2);
+  L.X3 = X.at(k, 4, 3);
+  L.V0 = U.at(k, 2, 0);
+  L.V1 = U.at(k, 2, 1);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) L.K[j] = K.at(k, 8, j);
+  L.k0 = kf.at(k, 2, 0);
+  L.k1 = kf.at(k, 2, 1);
+  load_ref(c, Xr, rf, k, L.r0, L.r1, L.r2);
+  load_uref(c, Ur, k, L.q0, L.q1);
+}
+
+// ---------------------------------------------------------------------------------------------
 // line search (core/ddp.py:256-301): all NA candidates advance together; returns the index of the
 // strictly smallest cost (first wins ties) or -1 if any candidate is non-finite.
 template <typename T, int NA>
@@ -130,28 +171,24 @@ __device__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>&
     Bc[a] = Bc0;
     J[a] = T(0);
   }
+  StepIn<T> cur, nxt;
+  load_step(cur, c, X, U, K, kf, Xr, rf, Ur, 0);
   for (int k = 0; k < N; ++k) {
-    T X0 = X.at(k, 4, 0), X1 = X.at(k, 4, 1), X2 = X.at(k, 4, 2), X3 = X.at(k, 4, 3);
-    T V0 = U.at(k, 2, 0), V1 = U.at(k, 2, 1);
-    T Kk[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) Kk[j] = K.at(k, 8, j);
-    T k0 = kf.at(k, 2, 0), k1 = kf.at(k, 2, 1);
-    T r0, r1, r2, q0, q1;
-    load_ref(c, Xr, rf, k, r0, r1, r2);
-    load_uref(c, Ur, k, q0, q1);
+    if (k + 1 < N) load_step(nxt, c, X, U, K, kf, Xr, rf, Ur, k + 1);
     T u0[NA], u1[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-      T e0 = a0[a] - X0, e1 = a1[a] - X1, e2 = a2[a] - X2, e3 = ab[a] - X3;
-      T du0 = k0 + (Kk[0] * e0 + Kk[1] * e1 + Kk[2] * e2 + Kk[3] * e3);
-      T du1 = k1 + (Kk[4] * e0 + Kk[5] * e1 + Kk[6] * e2 + Kk[7] * e3);
+      T e0 = a0[a] - cur.X0, e1 = a1[a] - cur.X1, e2 = a2[a] - cur.X2, e3 = ab[a] - cur.X3;
+      T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
+      T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
       T al = cfg.alphas[a];
-      u0[a] = clampv(V0 + al * du0, s.umin0, s.umax0);
-      u1[a] = clampv(V1 + al * du1, s.umin1, s.umax1);
-      J[a] = J[a] + stage_cost(c, a0[a], a1[a], a2[a], ab[a], u0[a], u1[a], r0, r1, r2, q0, q1);
+      u0[a] = clampv(cur.V0 + al * du0, s.umin0, s.umax0);
+      u1[a] = clampv(cur.V1 + al * du1, s.umin1, s.umax1);
+      J[a] = J[a] + stage_cost(c, a0[a], a1[a], a2[a], ab[a], u0[a], u1[a], cur.r0, cur.r1, cur.r2,
+                               cur.q0, cur.q1);
     }
     fhat_vec<T, NA>(s, a0, a1, a2, ab, u0, u1, Bc);
+    cur = nxt;
   }
   T r0, r1, r2;
   load_ref(c, Xr, rf, N, r0, r1, r2);
@@ -180,19 +217,19 @@ __device__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, co
                                  const Col<T>& U, const Col<T>& K, const Col<T>& kf) {
   const int N = s.N;
   T s0[1] = {x0[0]}, s1[1] = {x0[1]}, s2[1] = {x0[2]}, sb[1] = {x0[3]}, Bc[1] = {Bc0};
-  T o0 = X.at(0, 4, 0), o1 = X.at(0, 4, 1), o2 = X.at(0, 4, 2), o3 = X.at(0, 4, 3);
+  DCost<T> none;
+  none.kind = DTMPC_COST_TARGET;  // the references are not needed here
+  Col<T> nc = X;
+  StepIn<T> cur, nxt;
+  load_step(cur, none, X, U, K, kf, nc, 0, nc, 0);
   for (int k = 0; k < N; ++k) {
-    T n0 = X.at(k + 1, 4, 0), n1 = X.at(k + 1, 4, 1), n2 = X.at(k + 1, 4, 2), n3 = X.at(k + 1, 4, 3);
-    T V0 = U.at(k, 2, 0), V1 = U.at(k, 2, 1);
-    T Kk[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) Kk[j] = K.at(k, 8, j);
-    T k0 = kf.at(k, 2, 0), k1 = kf.at(k, 2, 1);
-    T e0 = s0[0] - o0, e1 = s1[0] - o1, e2 = s2[0] - o2, e3 = sb[0] - o3;
-    T du0 = k0 + (Kk[0] * e0 + Kk[1] * e1 + Kk[2] * e2 + Kk[3] * e3);
-    T du1 = k1 + (Kk[4] * e0 + Kk[5] * e1 + Kk[6] * e2 + Kk[7] * e3);
-    T u0[1] = {clampv(V0 + al * du0, s.umin0, s.umax0)};
-    T u1[1] = {clampv(V1 + al * du1, s.umin1, s.umax1)};
+    // the step-(k+1) load also fetches the OLD X[k+1] before this step overwrites it
+    if (k + 1 < N) load_step(nxt, none, X, U, K, kf, nc, 0, nc, k + 1);
+    T e0 = s0[0] - cur.X0, e1 = s1[0] - cur.X1, e2 = s2[0] - cur.X2, e3 = sb[0] - cur.X3;
+    T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
+    T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
+    T u0[1] = {clampv(cur.V0 + al * du0, s.umin0, s.umax0)};
+    T u1[1] = {clampv(cur.V1 + al * du1, s.umin1, s.umax1)};
     U.at(k, 2, 0) = u0[0];
     U.at(k, 2, 1) = u1[0];
     fhat_vec<T, 1>(s, s0, s1, s2, sb, u0, u1, Bc);
@@ -200,10 +237,7 @@ __device__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, co
     X.at(k + 1, 4, 1) = s1[0];
     X.at(k + 1, 4, 2) = s2[0];
     X.at(k + 1, 4, 3) = sb[0];
-    o0 = n0;
-    o1 = n1;
-    o2 = n2;
-    o3 = n3;
+    cur = nxt;
   }
 }
 

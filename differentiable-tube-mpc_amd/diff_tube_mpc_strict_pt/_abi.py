@@ -11,6 +11,7 @@ ABI_VERSION = 1
 MAX_OBS = 16
 MAX_ALPHAS = 8
 MAX_HORIZON = 512
+LOG_FIELDS = 18
 
 F32, F64 = 0, 1
 OBS_SMOOTHMIN, OBS_MIN, OBS_SINGLE, OBS_NONE = 0, 1, 2, 3

@@ -14,6 +14,9 @@ from . import _abi
 
 LIB_NAME = "libdtmpc.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# DTMPC_LIBRARY names an alternative build of the same ABI (e.g. a kernel variant from
+# ``build.py --variant``); it replaces the path, never adds a fallback.
+LIB_PATH = os.environ.get("DTMPC_LIBRARY", LIB_PATH)
 
 _lock = threading.Lock()
 _lib = None

@@ -75,7 +75,7 @@ class TubeMPC:
       disturbance: "philox" (device counter-based RNG keyed by global index and step) or "injected"
         (pass w to :meth:`step`).
       global_offset / global_batch: position of this shard in the global batch (multi-GPU).
-      write_log: keep the per-step record (x, u, xbar, ubar, b, L) on device.
+      write_log: keep the per-step record (x, u, xbar, ubar, b, L, gQ, gR, gqb) on device.
     """
 
     def __init__(self, setup, *, batch: int, device="cuda", dtype=torch.float32, disturbance: str = "philox",
@@ -128,11 +128,12 @@ class TubeMPC:
         self.n_partials = int(self.lib.dtmpc_tube_partials_count(B))
         self.partials = torch.zeros(self.n_partials, 8, **kw)
         self.sums = torch.zeros(8, **kw)
-        self.theta = torch.tensor(setup.theta0, **kw)
+        self._theta0 = torch.tensor(setup.theta0, **kw)
+        self.theta = self._theta0.clone()
         self.vel = torch.zeros(6, **kw)
         self.status = torch.zeros(B, dtype=torch.int32, device=self.device)
         self.iters = torch.zeros(2, B, dtype=torch.int32, device=self.device)
-        self.log = torch.zeros(12, B, **kw) if write_log else None
+        self.log = torch.zeros(_abi.LOG_FIELDS, B, **kw) if write_log else None
         self.t = 0
         st = _abi.DtmpcTubeState()
         st.x, st.b, st.xbar, st.bbar = (t.data_ptr() for t in (self.x, self.b, self.xbar, self.bbar))
@@ -163,7 +164,7 @@ class TubeMPC:
             self.Unom.copy_(U_nom0.to(self.Unom).permute(1, 2, 0))
         if U_aux0 is not None:
             self.Uaux.copy_(U_aux0.to(self.Uaux).permute(1, 2, 0))
-        self.theta.copy_(torch.tensor(self.setup.theta0, dtype=self.dtype))
+        self.theta.copy_(self._theta0)
         self.vel.zero_()
         self.status.zero_()
         self.t = 0
@@ -233,7 +234,7 @@ def run_closed_loop_experiment(cfg: Dict[str, Any], *, device: torch.device, run
     mpc.reset(x0)
     low = torch.tensor(setup.w_low, device=device, dtype=dtype)
     high = torch.tensor(setup.w_high, device=device, dtype=dtype)
-    logs = torch.zeros(H, 12, dtype=dtype, device=device)
+    logs = torch.zeros(H, _abi.LOG_FIELDS, dtype=dtype, device=device)
     thetas = torch.zeros(H, 6, dtype=dtype, device=device)
     probe = torch.empty(1, 3, device=device, dtype=dtype)
     for t in range(H):

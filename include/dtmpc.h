@@ -37,6 +37,7 @@ extern "C" {
 #define DTMPC_MAX_OBS 16
 #define DTMPC_MAX_ALPHAS 8
 #define DTMPC_MAX_HORIZON 512
+#define DTMPC_LOG_FIELDS 18 /* rows of dtmpc_tube_state.log */
 
 /* scalar type of the arrays */
 enum { DTMPC_F32 = 0, DTMPC_F64 = 1 };
@@ -147,7 +148,9 @@ typedef struct dtmpc_tube_state {
   void* work;       /* dtmpc_tube_workspace_bytes() scratch */
   const void* theta;/* [6] ancillary weights Qa(3), Ra(2), qba (shared by the batch) */
   void* partials;   /* [nblocks][8] per-workgroup sums: L, gQ(3), gR(2), gqb, pad */
-  void* log;        /* [12][B] or NULL: x(3) u(2) xbar(3) ubar(2) b L of step t */
+  void* log;        /* [18][B] or NULL: x(3) u(2) xbar(3) ubar(2) b L gQ(3) gR(2) gqb of step t
+                       (the gradient rows are the trajectory's own contribution before any
+                       status masking) */
   int32_t* status;  /* [B] DTMPC_ST_* bits (OR-accumulated) */
   int32_t* iters;   /* [2][B] nominal / ancillary iterations used, or NULL */
 } dtmpc_tube_state;

@@ -170,12 +170,12 @@ class Oracle:
     def tube_step(self, spec, tcfg, st: dict, theta, w=None, goff: int = 0, step: int = 0, want_log=True):
         """One Algorithm-2 step for every trajectory; `st` holds SoA numpy arrays (x [3,B], b [B],
         xbar, bbar, Xnom [N+1,4,B], Unom [N,2,B], Xaux, Uaux) updated in place.  Returns per-trajectory
-        [7, B] (L, gQ, gR, gqb), log [12, B], status [B], iters [2, B]."""
+        [7, B] (L, gQ, gR, gqb), log [18, B], status [B], iters [2, B]."""
         B = st["b"].shape[0]
         theta = self._a(theta)
         ws = None if w is None else np.ascontiguousarray(self._a(w).T)
         gout = np.zeros((7, B), self.dt)
-        log = np.zeros((12, B), self.dt) if want_log else None
+        log = np.zeros((18, B), self.dt) if want_log else None
         status = np.zeros(B, np.int32)
         iters = np.zeros((2, B), np.int32)
         for k in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux"):

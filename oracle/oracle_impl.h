@@ -964,7 +964,7 @@ void FN(oracle_doc_grad)(int N, long long B, const REAL* Xa, const REAL* Ua, con
 
 /* Algorithm-2 loop body per trajectory (core/tube_mpc.py:813-1023), theta read-only.
  * State arrays SoA as dtmpc_tube_state (host memory).  gout [7][B] per-trajectory L, gQ, gR, gqb.
- * log [12][B] (may be NULL).  w [3][B] (may be NULL when cfg->disturbance == 1). */
+ * log [18][B] (may be NULL).  w [3][B] (may be NULL when cfg->disturbance == 1). */
 void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long long B,
                           long long goff, long long step, REAL* x, REAL* b, REAL* xbar,
                           REAL* bbar, REAL* Xnom, REAL* Unom, REAL* Xaux, REAL* Uaux,
@@ -1047,7 +1047,7 @@ void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long 
         log[8 * B + i] = ub[0];
         log[9 * B + i] = ub[1];
         log[10 * B + i] = bs;
-        log[11 * B + i] = o[0];
+        for (int j = 0; j < 7; ++j) log[(long long)(11 + j) * B + i] = o[j];
       }
       for (int f = 0; f < 3; ++f) {
         x[(long long)f * B + i] = xhn[f] + ww[f];

@@ -1,0 +1,204 @@
+"""CPU tests of the drop-in boundary and the host logic: libdtmpc.so loads and exports exactly the
+symbols include/dtmpc.h declares, the ctypes structs match the C layout, argument validation happens
+before any device call, and the config -> typed-problem mapping follows the reference."""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from _common import config
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "dtmpc.h")
+
+
+def header_functions() -> set:
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?[\w]+[\s\*]+(dtmpc_\w+)\s*\(", src, flags=re.M))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from diff_tube_mpc_strict_pt import _lib
+
+    return _lib.load()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    from diff_tube_mpc_strict_pt import _abi
+
+    declared = header_functions()
+    assert len(declared) >= 15
+    missing = [n for n in declared if not hasattr(lib, n)]
+    assert not missing, missing
+    assert declared == set(_abi.PROTOTYPES), declared ^ set(_abi.PROTOTYPES)
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(REPO, "differentiable-tube-mpc_amd",
+                                                                        "diff_tube_mpc_strict_pt", "libdtmpc.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (dtmpc_\w+)", out))
+    assert declared <= exported
+    assert lib.dtmpc_abi_version() == _abi.ABI_VERSION
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """sizeof / offsetof of every ABI struct, compiled from include/dtmpc.h by gcc, vs the ctypes mirror."""
+    from diff_tube_mpc_strict_pt import _abi
+
+    structs = {"dtmpc_spec": _abi.DtmpcSpec, "dtmpc_cost": _abi.DtmpcCost, "dtmpc_ilqr_cfg": _abi.DtmpcIlqrCfg,
+               "dtmpc_adapt_cfg": _abi.DtmpcAdaptCfg, "dtmpc_tube_cfg": _abi.DtmpcTubeCfg,
+               "dtmpc_tube_state": _abi.DtmpcTubeState}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-o", str(exe), str(src)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        s, f, v = line.split()
+        got[(s, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == C.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
+
+
+def test_header_constants_match_ctypes_mirror():
+    from diff_tube_mpc_strict_pt import _abi
+
+    defines = dict(re.findall(r"^#define DTMPC_(\w+) (-?\d+)", open(HEADER).read(), flags=re.M))
+    checked = 0
+    for name, val in defines.items():
+        if hasattr(_abi, name):
+            assert getattr(_abi, name) == int(val), name
+            checked += 1
+    assert checked >= 5 and _abi.LOG_FIELDS == 18
+
+
+def test_arguments_validated_before_any_device_call(lib):
+    """Bad arguments return DTMPC_ERR_BAD_ARG with a message; no HIP call is made (safe without GPU)."""
+    from diff_tube_mpc_strict_pt import _abi
+    from diff_tube_mpc_strict_pt.core.problem import ILQRConfig, paper_config, paper_setup_from_config
+
+    st = paper_setup_from_config(paper_config())
+    spec, cost = st.problem.to_c(), st.nominal_cost.to_c()
+    cfg = st.ilqr_nom.to_c()
+    cfg.n_alphas = 0
+    rc = lib.dtmpc_ilqr_solve(_abi.F32, C.byref(spec), C.byref(cost), C.byref(cfg), 4, 1, None, None, 1, 1, 1, 1, None,
+                              1, None)
+    assert rc == _abi.ERR_BAD_ARG and b"n_alphas" in lib.dtmpc_last_error()
+    bad = st.problem.to_c()
+    bad.dbas_gamma = 1.5
+    rc = lib.dtmpc_dbas_rollout(_abi.F64, C.byref(bad), 4, 1, 1, 1, None)
+    assert rc == _abi.ERR_BAD_ARG and b"gamma" in lib.dtmpc_last_error()
+    track = st.nominal_cost.to_c()
+    track.kind = _abi.COST_TRACK
+    rc = lib.dtmpc_linearize(_abi.F32, C.byref(spec), C.byref(track), 4, 1, 1, None, None, 1, 1, 1, 1, None)
+    assert rc == _abi.ERR_BAD_ARG and b"Xref" in lib.dtmpc_last_error()
+    tc = _abi.DtmpcTubeCfg()
+    tc.nominal = cost
+    tc.nom_ilqr = st.ilqr_nom.to_c()
+    tc.aux_ilqr = ILQRConfig(horizon=50, line_search_alphas=(1.0, 0.5)).to_c()
+    state = _abi.DtmpcTubeState()
+    rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
+    assert rc == _abi.ERR_BAD_ARG and b"same width" in lib.dtmpc_last_error()
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536) == 4 * 50 * 20 * 65536
+    assert lib.dtmpc_tube_partials_count(65536) == 256
+    assert lib.dtmpc_sensitivity_workspace_bytes(_abi.F64, 50, 10, 1) == 8 * 10 * (50 * 20 + 51 * 20)
+
+
+def test_no_cpu_fallback():
+    """The product path refuses host tensors and a missing native library, loudly."""
+    import torch
+
+    from diff_tube_mpc_strict_pt import _lib
+    from diff_tube_mpc_strict_pt.core import TubeMPC, ilqr_solve
+    from diff_tube_mpc_strict_pt.core.problem import paper_config, paper_setup_from_config
+
+    st = paper_setup_from_config(paper_config())
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ilqr_solve(problem=st.problem, cost=st.nominal_cost, cfg=st.ilqr_nom, x0=torch.zeros(2, 4),
+                   V_init=torch.zeros(2, 50, 2))
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        TubeMPC(st, batch=4, device="cpu")
+    saved_lib, saved_path = _lib._lib, _lib.LIB_PATH
+    try:
+        _lib._lib, _lib.LIB_PATH = None, "/nonexistent/libdtmpc.so"
+        with pytest.raises(_lib.NativeLibraryError):
+            _lib.load()
+    finally:
+        _lib._lib, _lib.LIB_PATH = saved_lib, saved_path
+
+
+def test_paper_setup_follows_reference_wiring():
+    """core/tube_mpc.py:674-768: inverse barrier alpha = gamma = 0, 5 smooth-min circles, reg = 1e-6 (the
+    config's ilqr_reg is not used in paper mode), tol = 1e-3, theta0 = cost_auxiliary, Qf_aux = Qa."""
+    from diff_tube_mpc_strict_pt.core.problem import paper_config, paper_setup_from_config, tracking_cost
+
+    st = paper_setup_from_config(config())
+    assert st == paper_setup_from_config(paper_config())
+    p = st.problem
+    assert (p.barrier_type, p.dbas_alpha, p.dbas_gamma, p.dbas_eps) == ("inverse", 0.0, 0.0, 1e-4)
+    assert p.obs_aggregation == "smoothmin" and len(p.obstacles) == 5 and p.obs_beta == 20.0
+    assert p.u_min == (-10.0, -math.pi) and p.u_max == (10.0, math.pi)
+    assert st.ilqr_nom.reg == 1e-6 and st.ilqr_nom.tol == 1e-3 and st.ilqr_nom.max_iter == 10
+    assert st.ilqr_aux.max_iter == 20 and len(st.ilqr_aux.line_search_alphas) == 7
+    assert st.theta0 == (1.0, 1.0, 1.0, 1.0, 1.0, 1.0)
+    assert st.adapt.lr_eta == 0.05 and st.adapt.momentum == 0.9
+    tc = tracking_cost((1, 2, 3, 4, 5, 6))
+    assert tc.Qf == tc.Q == (1.0, 2.0, 3.0) and tc.kind == "track"
+    c = tc.to_c()
+    assert list(c.Qf) == [1.0, 2.0, 3.0] and c.qb == 6.0
+
+
+def test_problem_validation_mirrors_reference_errors():
+    import dataclasses
+
+    from diff_tube_mpc_strict_pt.core.problem import ILQRConfig, problem_from_config
+
+    base = problem_from_config(config())
+    with pytest.raises(ValueError, match="gamma"):
+        dataclasses.replace(base, dbas_gamma=1.2)  # core/barrier.py:90-91
+    with pytest.raises(ValueError, match="alpha"):
+        dataclasses.replace(base, dbas_alpha=-0.1)  # core/barrier.py:43-44
+    with pytest.raises(ValueError, match="barrier_type"):
+        dataclasses.replace(base, barrier_type="quadratic")  # core/barrier.py:72
+    with pytest.raises(ValueError):
+        ILQRConfig(horizon=50, line_search_alphas=tuple([1.0] * 9)).to_c()
+    single = problem_from_config({**config(), "environment": {"obstacle": {"center": [5, 5], "radius": 1.5}}})
+    assert single.obs_aggregation == "single" and single.obstacles[0].radius == 1.5
+
+
+def test_shard_range_partitions_global_batch():
+    from diff_tube_mpc_strict_pt.core import shard_range
+
+    for Bg in (1, 7, 4096, 65536, 65537):
+        for W in (1, 2, 3, 8):
+            if Bg < W:
+                continue
+            parts = [shard_range(Bg, r, W) for r in range(W)]
+            assert parts[0][0] == 0 and parts[-1][1] == Bg
+            assert all(parts[r][1] == parts[r + 1][0] for r in range(W - 1))
+            sizes = [hi - lo for lo, hi in parts]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)
+
+
+def test_philox_stream_is_keyed_by_global_index(oracle_lib):
+    a = oracle_lib.philox_bits(0, 5, 3)
+    assert not np.array_equal(a, oracle_lib.philox_bits(0, 6, 3))
+    assert not np.array_equal(a, oracle_lib.philox_bits(0, 5, 4))
+    assert not np.array_equal(a, oracle_lib.philox_bits(1, 5, 3))
+    assert np.array_equal(a, oracle_lib.philox_bits(0, 5, 3))

@@ -274,7 +274,7 @@ def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode):
     B = 700
     rng = np.random.default_rng(11)
     x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(npdt)
-    mpc = TubeMPC(st, batch=B, device=dev, dtype=tdt, disturbance="philox", seed=3)
+    mpc = TubeMPC(st, batch=B, device=dev, dtype=tdt, disturbance="philox", seed=3, write_log=True)
     mpc.reset(_t(x, tdt, dev))
     ors = oracles(npdt)
     base = 1e-9 if tag == "f64" else 1e-4
@@ -293,7 +293,7 @@ def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode):
             sums = np.zeros(8, npdt)
             sums[:7] = gout.sum(1)
             theta, _ = o.theta_update(st.adapt.to_c(), 1.0 / B, sums, th0, vel0)
-            outs.append((state, theta, so))
+            outs.append((state, theta, so, gout))
         keep = (mpc.status.cpu().numpy() == 0) & (outs[0][2] == 0)
         assert keep.mean() > 0.99
         for k in ("x", "xbar", "b"):
@@ -306,10 +306,23 @@ def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode):
             dev_k = np.transpose(getattr(mpc, k).cpu().numpy(), (2, 0, 1))[keep]
             frac, e, s = agreement(dev_k, [np.transpose(o_[0][k], (2, 0, 1))[keep] for o_ in outs], base)
             assert frac >= need, (t, k, frac, np.sort(e)[-5:])
+        # per-trajectory DOC loss + gradient rows [L, gQ(3), gR(2), gqb] (log rows 11..17)
+        log = mpc.log.cpu().numpy()
+        frac, e, s = agreement(log[11:18].T[keep], [o_[3].T[keep] for o_ in outs], base)
+        assert frac >= need, (t, "grad", frac, np.sort(e)[-5:])
+        # shared theta: momentum + projection applied to the device's own batch sums.  (Comparing it
+        # with the oracle's theta instead would be a lottery: the batch mean is dominated by the few
+        # obstacle-grazing trajectories whose gradients are chaotic -- the three CPU builds' thetas
+        # already differ by up to 3e4 relative on this batch.)
+        g = np.where(mpc.status.cpu().numpy() == 0, log[11:18], 0).astype(np.float64)
+        sums = np.zeros(8)
+        sums[:7] = g.sum(1)
+        th_ref, _ = ors[0].theta_update(st.adapt.to_c(), 1.0 / B, sums.astype(npdt), th0, vel0)
         th = mpc.theta.cpu().numpy()
-        ths = [o_[1] for o_ in outs]
-        tol = max(base, 10 * max(rel(x_, ths[0]) for x_ in ths[1:]))
-        assert min(rel(th, x_) for x_ in ths) < tol, (t, th, ths)
+        eta = st.adapt.lr_eta
+        scale = np.abs(th0) + eta * (np.abs(vel0) + np.abs(g).sum(1)[1:] / B) + 1e-30
+        tol_th = 1e-12 if tag == "f64" else 1e-5
+        assert (np.abs(th - th_ref) <= tol_th * scale).all(), (t, th, th_ref)
 
 
 def _tube_cfg(st, seed):
