@@ -53,6 +53,37 @@ __device__ __forceinline__ T wrap_angle(T e) {  // run_nominal.py:32-34
 }
 
 // ---------------------------------------------------------------------------------------------
+// Phase timers for profiling builds only (build.py --variant prof -D DTMPC_PROFILE): per-lane
+// s_memtime deltas accumulated per phase, summed by lane 0 of every wave into g_prof.  In product
+// builds Prof is empty and every call folds away.
+#ifdef DTMPC_PROFILE
+__device__ unsigned long long g_prof[16];
+struct Prof {
+  unsigned long long acc[12], last;
+  __device__ __forceinline__ void start() {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) acc[i] = 0;
+    last = __builtin_readcyclecounter();
+  }
+  __device__ __forceinline__ void mark(int i) {
+    unsigned long long t = __builtin_readcyclecounter();
+    acc[i] += t - last;
+    last = t;
+  }
+  __device__ __forceinline__ void flush() {
+    if ((threadIdx.x & 63) == 0)
+      for (int i = 0; i < 12; ++i) atomicAdd(&g_prof[i], acc[i]);
+  }
+};
+#else
+struct Prof {
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void flush() {}
+};
+#endif
+
+// ---------------------------------------------------------------------------------------------
 // typed problem description (built on the host from dtmpc_spec / dtmpc_cost / dtmpc_ilqr_cfg)
 template <typename T>
 struct DSpec {
@@ -103,8 +134,9 @@ __device__ __forceinline__ T h_circle(const DSpec<T>& s, int i, T px, T py) {  /
 //   smoothmin: h_multi_circle_obstacles :41-69 (stable LSE, two passes)
 //   min:       h_min_circle_obstacles :95-106
 //   single:    h_circle_obstacle :16-30;  none: 1 (run_nominal.py:256)
-// The W-wide value path stays two-pass: holding all z_i for W points in registers (tried, round 1)
-// pushed the fused tube kernel into AGPR spills and scratch.  h_grad (W = 1) keeps z_i in registers.
+// The value path keeps a runtime obstacle loop: specialising it on a compile-time count (tried in
+// round 1, both as register-held z_i and as recomputed passes) made the compiler copy the by-value
+// spec to scratch and tripled the line-search cost.  h_grad (W = 1) is specialised below.
 constexpr int kFastObs = 8;
 
 template <typename T, int W>
@@ -151,31 +183,46 @@ __device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* p
 // h and dh/d(px,py) at one point (grad_h_multi_circle_obstacles :72-92,
 // grad_h_min_circle_obstacles :109-117, grad_h_circle_obstacle :33-38).  The softmax weights are
 // e_i * (1/sum e) instead of e_i / sum e (one reciprocal per point).
+template <typename T, int MO>
+__device__ __forceinline__ T h_grad_fixed(const DSpec<T>& s, T px, T py, T& gx, T& gy) {
+  // no contraction: z_i = -beta h_i is rounded before z_i - zmax, as in the reference (a fused
+  // fma(-beta, h_i, -zmax) shifts f32 plans measurably on knife-edge golden cases)
+#ifndef DTMPC_HGRAD_CONTRACT
+#pragma clang fp contract(off)
+#endif
+  T z[MO], zmax = T(0);
+#pragma unroll
+  for (int i = 0; i < MO; ++i) {
+    z[i] = s.neg_beta * h_circle(s, i, px, py);
+    zmax = (i == 0 || z[i] > zmax) ? z[i] : zmax;
+  }
+  T se = T(0), sx = T(0), sy = T(0);
+#pragma unroll
+  for (int i = 0; i < MO; ++i) {
+    T e = m_exp(z[i] - zmax);
+    se += e;
+    sx += e * (T(2) * (px - s.cx[i]));
+    sy += e * (T(2) * (py - s.cy[i]));
+  }
+  T inv = m_rcp(se);
+  gx = sx * inv;
+  gy = sy * inv;
+  return s.neg_inv_beta * (zmax + m_log(se));
+}
+
 template <typename T>
 __device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy) {
   if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0 && s.M <= kFastObs) {
-    T z[kFastObs], zmax = T(0);
-#pragma unroll
-    for (int i = 0; i < kFastObs; ++i) {
-      if (i < s.M) {
-        z[i] = s.neg_beta * h_circle(s, i, px, py);
-        zmax = (i == 0 || z[i] > zmax) ? z[i] : zmax;
-      }
+    switch (s.M) {  // wave-uniform
+      case 1: return h_grad_fixed<T, 1>(s, px, py, gx, gy);
+      case 2: return h_grad_fixed<T, 2>(s, px, py, gx, gy);
+      case 3: return h_grad_fixed<T, 3>(s, px, py, gx, gy);
+      case 4: return h_grad_fixed<T, 4>(s, px, py, gx, gy);
+      case 5: return h_grad_fixed<T, 5>(s, px, py, gx, gy);
+      case 6: return h_grad_fixed<T, 6>(s, px, py, gx, gy);
+      case 7: return h_grad_fixed<T, 7>(s, px, py, gx, gy);
+      default: return h_grad_fixed<T, 8>(s, px, py, gx, gy);
     }
-    T se = T(0), sx = T(0), sy = T(0);
-#pragma unroll
-    for (int i = 0; i < kFastObs; ++i) {
-      if (i < s.M) {
-        T e = m_exp(z[i] - zmax);
-        se += e;
-        sx += e * (T(2) * (px - s.cx[i]));
-        sy += e * (T(2) * (py - s.cy[i]));
-      }
-    }
-    T inv = m_rcp(se);
-    gx = sx * inv;
-    gy = sy * inv;
-    return s.neg_inv_beta * (zmax + m_log(se));
   }
   if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0) {
     T zmax = s.neg_beta * h_circle(s, 0, px, py);

@@ -178,8 +178,11 @@ __global__ void __launch_bounds__(kBlock) ilqr_kernel(DSpec<T> s, DCost<T> c, DI
   Col<T> cx0 = col<T>(x0p, i, B);
   T x0[4] = {cx0.at(0, 4, 0), cx0.at(0, 4, 1), cx0.at(0, 4, 2), cx0.at(0, 4, 3)};
   int it = 0;
+  Prof pr;
+  pr.start();
   int st = ilqr_traj<T, NA>(s, c, cfg, x0, col<T>(Xp, i, B), col<T>(Up, i, B), col<T>(Kp, i, B),
-                            col<T>(kfp, i, B), col<T>(Xrp, i, B), 3, col<T>(Urp, i, B), it);
+                            col<T>(kfp, i, B), col<T>(Xrp, i, B), 3, col<T>(Urp, i, B), it, pr, 0);
+  pr.flush();
   if (iters) iters[i] = it;
   if (status) status[i] |= st;
 }
@@ -296,7 +299,9 @@ __global__ void __launch_bounds__(kBlock) tube_step_kernel(DSpec<T> s, DCost<T> 
     // nominal MPC solve (fixed weights) :813-857
     T xn0[4] = {y0, y1, y2, yb};
     Col<T> none = col<T>((void*)nullptr, i, B);
-    st |= ilqr_traj<T, NA>(s, cn, cfn, xn0, Xn, Un, K, kf, none, 0, none, itn);
+    Prof pr;
+    pr.start();
+    st |= ilqr_traj<T, NA>(s, cn, cfn, xn0, Xn, Un, K, kf, none, 0, none, itn, pr, 0);
     // ancillary MPC tracking the nominal plan :863-909 (terminal weight Qa, :885, :891)
     DCost<T> ca;
     ca.kind = DTMPC_COST_TRACK;
@@ -309,10 +314,13 @@ __global__ void __launch_bounds__(kBlock) tube_step_kernel(DSpec<T> s, DCost<T> 
     ca.qb = a.theta[5];
     ca.t0 = ca.t1 = ca.t2 = T(0);
     T xa0[4] = {x0, x1, x2, xb};
-    st |= ilqr_traj<T, NA>(s, ca, cfa, xa0, Xa, Ua, K, kf, Xn, 4, Un, ita);
+    pr.mark(8);
+    st |= ilqr_traj<T, NA>(s, ca, cfa, xa0, Xa, Ua, K, kf, Xn, 4, Un, ita, pr, 4);
+    pr.mark(8);
     // upper loss, DOC sensitivity and analytic gradient :915-976
     st |= sens_traj<T, false, false, true>(s, ca, Xa, Ua, Xn, 4, Un, Xn, 4, K, kf, AB, none, none,
                                            none, none, acc);
+    pr.mark(9);
     // plant step with disturbance, nominal propagation :990-1001
     T u0 = Ua.at(0, 2, 0), u1 = Ua.at(0, 2, 1);
     T v0 = Un.at(0, 2, 0), v1 = Un.at(0, 2, 1);
@@ -380,6 +388,8 @@ __global__ void __launch_bounds__(kBlock) tube_step_kernel(DSpec<T> s, DCost<T> 
       a.iters[i] = itn;
       a.iters[nb + i] = ita;
     }
+    pr.mark(10);
+    pr.flush();
   }
   // fixed-order workgroup sum of [L, gQ, gR, gqb]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -563,6 +573,20 @@ static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B
 using namespace dtmpc;
 
 extern "C" {
+
+#ifdef DTMPC_PROFILE
+// profiling builds only (not part of include/dtmpc.h): read / clear the phase-cycle accumulators
+int dtmpc_prof_read(void* host16) {
+  return hipMemcpyFromSymbol(host16, HIP_SYMBOL(dtmpc::g_prof), 16 * sizeof(unsigned long long)) ==
+                 hipSuccess
+             ? 0
+             : 1;
+}
+int dtmpc_prof_reset(void) {
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(dtmpc::g_prof), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int dtmpc_abi_version(void) { return DTMPC_ABI_VERSION; }
 

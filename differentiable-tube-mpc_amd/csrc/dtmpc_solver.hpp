@@ -46,6 +46,35 @@ __device__ __forceinline__ void load_uref(const DCost<T>& c, const Col<T>& Ur, i
 }
 
 // ---------------------------------------------------------------------------------------------
+// Software prefetch depth of the step loops.  At the benchmark batch there is exactly one wave per
+// SIMD, so no other wave hides HBM latency: every pass keeps the loads of the next kPrefetch steps
+// in flight (stores share vmcnt with loads on gfx9-family parts, so loads are issued ahead of them).
+#ifndef DTMPC_PREFETCH
+#define DTMPC_PREFETCH 1
+#endif
+constexpr int kPrefetch = DTMPC_PREFETCH;
+
+// Everything the backward pass reads at step k: tape X[k], V[k] and the tracking references.
+template <typename T>
+struct BackIn {
+  T X0, X1, X2, X3, V0, V1, r0, r1, r2, q0, q1;
+};
+
+template <typename T>
+__device__ __forceinline__ void load_back(BackIn<T>& L, const DCost<T>& c, const Col<T>& X,
+                                          const Col<T>& U, const Col<T>& Xr, int rf, const Col<T>& Ur,
+                                          int k) {
+  L.X0 = X.at(k, 4, 0);
+  L.X1 = X.at(k, 4, 1);
+  L.X2 = X.at(k, 4, 2);
+  L.X3 = X.at(k, 4, 3);
+  L.V0 = U.at(k, 2, 0);
+  L.V1 = U.at(k, 2, 1);
+  load_ref(c, Xr, rf, k, L.r0, L.r1, L.r2);
+  load_uref(c, Ur, k, L.q0, L.q1);
+}
+
+// ---------------------------------------------------------------------------------------------
 // backward pass (core/ddp.py:172-254): linearise along (X, U) and run the Riccati recursion,
 // writing K [N][8], kff [N][2].  grad h / B' at x_{k+1} are carried from step k+1 (the reference
 // recomputes x_{k+1} = f(x_k, u_k) inside dubins_augmented_jacobian; it is the tape's X[k+1]).
@@ -74,26 +103,21 @@ __device__ bool ilqr_backward(const DSpec<T>& s, const DCost<T>& c, T reg, const
   T hn = h_grad(s, xn0, xn1, gxn, gyn);
   T dBn = dbarrier_relaxed(s, hn);
   bool ok = finite(R.Vx[0]) && finite(R.Vx[1]) && finite(R.Vx[2]) && finite(R.Vx[3]);
-  // prefetched step inputs (x_k, u_k, references), one step ahead of the recursion
-  T p0 = X.at(N - 1, 4, 0), p1 = X.at(N - 1, 4, 1), p2 = X.at(N - 1, 4, 2), pb = X.at(N - 1, 4, 3);
-  T pu0 = U.at(N - 1, 2, 0), pu1 = U.at(N - 1, 2, 1), pr0, pr1, pr2, pq0, pq1;
-  load_ref(c, Xr, rf, N - 1, pr0, pr1, pr2);
-  load_uref(c, Ur, N - 1, pq0, pq1);
+  // step inputs (x_k, u_k, references) prefetched kPrefetch steps ahead of the recursion
+  BackIn<T> q[kPrefetch];
+#pragma unroll
+  for (int j = 0; j < kPrefetch; ++j)
+    if (N - 1 - j >= 0) load_back(q[j], c, X, U, Xr, rf, Ur, N - 1 - j);
   for (int k = N - 1; k >= 0; --k) {
-    T x0 = p0, x1 = p1, x2 = p2, xb = pb, u0 = pu0, u1 = pu1, q0 = pq0, q1 = pq1;
-    r0 = pr0;
-    r1 = pr1;
-    r2 = pr2;
-    if (k > 0) {
-      p0 = X.at(k - 1, 4, 0);
-      p1 = X.at(k - 1, 4, 1);
-      p2 = X.at(k - 1, 4, 2);
-      pb = X.at(k - 1, 4, 3);
-      pu0 = U.at(k - 1, 2, 0);
-      pu1 = U.at(k - 1, 2, 1);
-      load_ref(c, Xr, rf, k - 1, pr0, pr1, pr2);
-      load_uref(c, Ur, k - 1, pq0, pq1);
-    }
+    const BackIn<T> cur = q[0];
+#pragma unroll
+    for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
+    if (k - kPrefetch >= 0) load_back(q[kPrefetch - 1], c, X, U, Xr, rf, Ur, k - kPrefetch);
+    const T x0 = cur.X0, x1 = cur.X1, x2 = cur.X2, xb = cur.X3, u0 = cur.V0, u1 = cur.V1, q0 = cur.q0,
+            q1 = cur.q1;
+    r0 = cur.r0;
+    r1 = cur.r1;
+    r2 = cur.r2;
     T sn, cs;
     m_sincos(x2, &sn, &cs);
     T gxk, gyk;
@@ -171,10 +195,15 @@ __device__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>&
     Bc[a] = Bc0;
     J[a] = T(0);
   }
-  StepIn<T> cur, nxt;
-  load_step(cur, c, X, U, K, kf, Xr, rf, Ur, 0);
+  StepIn<T> q[kPrefetch];
+#pragma unroll
+  for (int j = 0; j < kPrefetch; ++j)
+    if (j < N) load_step(q[j], c, X, U, K, kf, Xr, rf, Ur, j);
   for (int k = 0; k < N; ++k) {
-    if (k + 1 < N) load_step(nxt, c, X, U, K, kf, Xr, rf, Ur, k + 1);
+    const StepIn<T> cur = q[0];
+#pragma unroll
+    for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
+    if (k + kPrefetch < N) load_step(q[kPrefetch - 1], c, X, U, K, kf, Xr, rf, Ur, k + kPrefetch);
     T u0[NA], u1[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
@@ -188,7 +217,6 @@ __device__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>&
                                cur.q0, cur.q1);
     }
     fhat_vec<T, NA>(s, a0, a1, a2, ab, u0, u1, Bc);
-    cur = nxt;
   }
   T r0, r1, r2;
   load_ref(c, Xr, rf, N, r0, r1, r2);
@@ -220,11 +248,16 @@ __device__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, co
   DCost<T> none;
   none.kind = DTMPC_COST_TARGET;  // the references are not needed here
   Col<T> nc = X;
-  StepIn<T> cur, nxt;
-  load_step(cur, none, X, U, K, kf, nc, 0, nc, 0);
+  StepIn<T> q[kPrefetch];
+#pragma unroll
+  for (int j = 0; j < kPrefetch; ++j)
+    if (j < N) load_step(q[j], none, X, U, K, kf, nc, 0, nc, j);
   for (int k = 0; k < N; ++k) {
-    // the step-(k+1) load also fetches the OLD X[k+1] before this step overwrites it
-    if (k + 1 < N) load_step(nxt, none, X, U, K, kf, nc, 0, nc, k + 1);
+    // the prefetch also fetches the OLD X[k+j] before step k+j-1 overwrites it
+    const StepIn<T> cur = q[0];
+#pragma unroll
+    for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
+    if (k + kPrefetch < N) load_step(q[kPrefetch - 1], none, X, U, K, kf, nc, 0, nc, k + kPrefetch);
     T e0 = s0[0] - cur.X0, e1 = s1[0] - cur.X1, e2 = s2[0] - cur.X2, e3 = sb[0] - cur.X3;
     T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
     T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
@@ -237,7 +270,6 @@ __device__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, co
     X.at(k + 1, 4, 1) = s1[0];
     X.at(k + 1, 4, 2) = s2[0];
     X.at(k + 1, 4, 3) = sb[0];
-    cur = nxt;
   }
 }
 
@@ -267,7 +299,8 @@ __device__ void rollout_traj(const DSpec<T>& s, const T* x0, const Col<T>& X, co
 template <typename T, int NA>
 __device__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, const T* x0,
                          const Col<T>& X, const Col<T>& U, const Col<T>& K, const Col<T>& kf,
-                         const Col<T>& Xr, int rf, const Col<T>& Ur, int& iters) {
+                         const Col<T>& Xr, int rf, const Col<T>& Ur, int& iters, Prof& pr,
+                         int pb) {
   const int N = s.N;
   // V = clamp(V_init); X = rollout(x0, V)   (:127-131)
   for (int k = 0; k < N; ++k) {
@@ -276,17 +309,21 @@ __device__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& c
   }
   rollout_traj(s, x0, X, U);
   T Bc0 = barrier_of_state(s, x0[0], x0[1]);
+  pr.mark(pb + 0);
   bool have_prev = false;
   T prev = T(0);
   iters = 0;
   for (int it = 0; it < cfg.max_iter; ++it) {
     iters = it + 1;
     if (!ilqr_backward(s, c, cfg.reg, X, U, K, kf, Xr, rf, Ur)) return DTMPC_ST_NONFINITE;
+    pr.mark(pb + 1);
     T bestJ;
     int best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, K, kf, Xr, rf, Ur, bestJ);
+    pr.mark(pb + 2);
     if (best < 0) return DTMPC_ST_NONFINITE;
     T al = cfg.alphas[best];
     if (al != T(0)) commit_candidate(s, al, x0, Bc0, X, U, K, kf);
+    pr.mark(pb + 3);
     // :303-305
     if (have_prev && m_abs(prev - bestJ) < cfg.tol) break;
     have_prev = true;

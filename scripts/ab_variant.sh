@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
-# A/B a kernel variant on the GPU box: GPU parity tests + quick bench with the product library and with
-# libdtmpc_<variant>.so (build.py --variant).  usage: bash scripts/ab_variant.sh VARIANT [pytest -k expr]
+# A/B kernel variants on the GPU box: GPU parity tests + quick bench with the product library and with
+# each libdtmpc_<variant>.so (build.py --variant).  usage: bash scripts/ab_variant.sh "V1 V2" [pytest -k expr]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 V=$1
@@ -17,7 +17,9 @@ step() {  # name seconds cmd...
 KARG=(); [ -n "$K" ] && KARG=(-k "$K")
 step tests_base 900 python -m pytest tests -m gpu -q -rf "${KARG[@]}"
 step bench_base 300 python bench.py --steps 5 --warmup 1 --no-cpu
-export DTMPC_LIBRARY=$PWD/$LIBDIR/libdtmpc_$V.so
-step tests_$V 900 python -m pytest tests -m gpu -q -rf "${KARG[@]}"
-step bench_$V 300 python bench.py --steps 5 --warmup 1 --no-cpu
+for v in $V; do
+  export DTMPC_LIBRARY=$PWD/$LIBDIR/libdtmpc_$v.so
+  step tests_$v 900 python -m pytest tests -m gpu -q -rf "${KARG[@]}"
+  step bench_$v 300 python bench.py --steps 5 --warmup 1 --no-cpu
+done
 exit 0

@@ -1,0 +1,46 @@
+"""Phase cycle breakdown of the fused tube step from a profiling build (libdtmpc_prof.so, built with
+python differentiable-tube-mpc_amd/build.py --variant prof -D DTMPC_PROFILE).  Prints, per phase, the
+mean s_memtime cycles per wave and the share of the wave lifetime.
+usage: DTMPC_LIBRARY=.../libdtmpc_prof.so python scripts/phase_prof.py [--batch B]"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "differentiable-tube-mpc_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from bench import bench_setup, initial_states  # noqa: E402
+from diff_tube_mpc_strict_pt import _lib  # noqa: E402
+from diff_tube_mpc_strict_pt.core import TubeMPC  # noqa: E402
+
+NAMES = ["nom.init", "nom.backward", "nom.linesearch", "nom.commit", "aux.init", "aux.backward",
+         "aux.linesearch", "aux.commit", "misc", "sens+grad", "plant+shift"]
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=65536)
+a = ap.parse_args()
+lib = _lib.load()
+lib.dtmpc_prof_read.argtypes = [C.c_void_p]
+st = bench_setup("f32")
+mpc = TubeMPC(st, batch=a.batch, device="cuda", dtype=torch.float32, disturbance="philox", seed=0)
+x0 = initial_states(0, a.batch, "cuda", torch.float32)
+mpc.reset(x0)
+mpc.step()
+torch.cuda.synchronize()
+lib.dtmpc_prof_reset()
+mpc.reset(x0)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+mpc.step(kernel_events=(e0, e1))
+torch.cuda.synchronize()
+buf = np.zeros(16, np.uint64)
+assert lib.dtmpc_prof_read(buf.ctypes.data) == 0
+waves = a.batch // 64
+cyc = buf[:11].astype(np.float64) / waves
+tot = cyc.sum()
+print(f"kernel {e0.elapsed_time(e1):.3f} ms; per-wave total {tot:.4g} cycles")
+for n, c in zip(NAMES, cyc):
+    print(f"{n:16s} {c:12.4g} cyc/wave {100 * c / tot:6.1f} %")
+print("per step-pass (N=50): nom.backward/it %.0f, nom.ls/it %.0f, nom.commit/it %.0f cycles" %
+      (cyc[1] / 10 / 50, cyc[2] / 10 / 50, cyc[3] / 10 / 50))
