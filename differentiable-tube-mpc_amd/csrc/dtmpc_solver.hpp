@@ -79,7 +79,7 @@ __device__ __forceinline__ void load_back(BackIn<T>& L, const DCost<T>& c, const
 // writing K [N][8], kff [N][2].  grad h / B' at x_{k+1} are carried from step k+1 (the reference
 // recomputes x_{k+1} = f(x_k, u_k) inside dubins_augmented_jacobian; it is the tape's X[k+1]).
 template <typename T>
-__device__ bool ilqr_backward(const DSpec<T>& s, const DCost<T>& c, T reg, const Col<T>& X,
+__device__ __forceinline__ bool ilqr_backward(const DSpec<T>& s, const DCost<T>& c, T reg, const Col<T>& X,
                               const Col<T>& U, const Col<T>& K, const Col<T>& kf,
                               const Col<T>& Xr, int rf, const Col<T>& Ur) {
   const int N = s.N;
@@ -180,7 +180,7 @@ __device__ __forceinline__ void load_step(StepIn<T>& L, const DCost<T>& c, const
 // line search (core/ddp.py:256-301): all NA candidates advance together; returns the index of the
 // strictly smallest cost (first wins ties) or -1 if any candidate is non-finite.
 template <typename T, int NA>
-__device__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg,
+__device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg,
                            const T* x0, T Bc0, const Col<T>& X, const Col<T>& U, const Col<T>& K,
                            const Col<T>& kf, const Col<T>& Xr, int rf, const Col<T>& Ur,
                            T& bestJ) {
@@ -241,7 +241,7 @@ __device__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>&
 // Materialise the chosen candidate in place: X, U <- rollout with step alpha (same arithmetic
 // as the candidate lane of line_search).  X[k+1] of the old tape is read before it is replaced.
 template <typename T>
-__device__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, const Col<T>& X,
+__device__ __forceinline__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, const Col<T>& X,
                                  const Col<T>& U, const Col<T>& K, const Col<T>& kf) {
   const int N = s.N;
   T s0[1] = {x0[0]}, s1[1] = {x0[1]}, s2[1] = {x0[2]}, sb[1] = {x0[3]}, Bc[1] = {Bc0};
@@ -275,7 +275,7 @@ __device__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, co
 
 // rollout core/ddp.py:89-99 (U used as stored)
 template <typename T>
-__device__ void rollout_traj(const DSpec<T>& s, const T* x0, const Col<T>& X, const Col<T>& U) {
+__device__ __forceinline__ void rollout_traj(const DSpec<T>& s, const T* x0, const Col<T>& X, const Col<T>& U) {
   const int N = s.N;
   T s0[1] = {x0[0]}, s1[1] = {x0[1]}, s2[1] = {x0[2]}, sb[1] = {x0[3]};
   T Bc[1] = {barrier_of_state(s, x0[0], x0[1])};
@@ -297,7 +297,7 @@ __device__ void rollout_traj(const DSpec<T>& s, const T* x0, const Col<T>& X, co
 // iLQR for one trajectory (core/ddp.py:102-307).  U: in V_init, out V*.  X: out X*.
 // K/kf: scratch + gains of the last backward pass.  Returns DTMPC_ST_* bits.
 template <typename T, int NA>
-__device__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, const T* x0,
+__device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, const T* x0,
                          const Col<T>& X, const Col<T>& U, const Col<T>& K, const Col<T>& kf,
                          const Col<T>& Xr, int rf, const Col<T>& Ur, int& iters, Prof& pr,
                          int pb) {
@@ -340,7 +340,7 @@ __device__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& c
 // GRAD: accumulate the upper loss and the analytic DOC gradient (core/tube_mpc.py:915-976) into
 // acc[7] = L, gQ(3), gR(2), gqb with du = U - Ur.
 template <typename T, bool LAMBDA, bool OUT, bool GRAD>
-__device__ int sens_traj(const DSpec<T>& s, const DCost<T>& c, const Col<T>& X, const Col<T>& U,
+__device__ __forceinline__ int sens_traj(const DSpec<T>& s, const DCost<T>& c, const Col<T>& X, const Col<T>& U,
                          const Col<T>& Xr, int rf, const Col<T>& Ur, const Col<T>& Xb, int rfb,
                          const Col<T>& K, const Col<T>& kf, const Col<T>& AB, const Col<T>& VV,
                          const Col<T>& dX, const Col<T>& dU, const Col<T>& dL, T* acc) {
