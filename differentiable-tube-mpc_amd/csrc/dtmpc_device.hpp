@@ -34,6 +34,8 @@ __device__ __forceinline__ float m_rcp(float x) { return __builtin_amdgcn_rcpf(x
 __device__ __forceinline__ double m_rcp(double x) { return 1.0 / x; }
 __device__ __forceinline__ float m_atan2(float y, float x) { return atan2f(y, x); }
 __device__ __forceinline__ double m_atan2(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ float m_min(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ double m_min(double a, double b) { return __builtin_fmin(a, b); }
 __device__ __forceinline__ float m_abs(float x) { return fabsf(x); }
 __device__ __forceinline__ double m_abs(double x) { return fabs(x); }
 template <typename T>
@@ -123,11 +125,21 @@ struct Col {
 // ---------------------------------------------------------------------------------------------
 // safety function h  (core/systems/dubins_obstacles.py)
 
+// Obstacle parameters are read in place from the kernarg segment: every kernel that takes a spec
+// takes it BY VALUE AS ITS FIRST PARAMETER, so it sits at offset 0 of the (read-only, wave-uniform)
+// kernarg block.  Indexing the by-value copy `s.cx[i]` with a runtime i instead makes the compiler
+// materialise the whole spec in scratch once the kernel also has compile-time-indexed paths.
 template <typename T>
-__device__ __forceinline__ T h_circle(const DSpec<T>& s, int i, T px, T py) {  // :16-30
-  T dx = px - s.cx[i];
-  T dy = py - s.cy[i];
-  return dx * dx + dy * dy - s.r2[i];
+__device__ __forceinline__ const DSpec<T>& kspec() {
+  return *(const DSpec<T>*)(__builtin_amdgcn_kernarg_segment_ptr());  // addrspace(4) -> generic
+}
+
+template <typename T>
+__device__ __forceinline__ T h_circle(const DSpec<T>&, int i, T px, T py) {  // :16-30
+  const DSpec<T>& k = kspec<T>();
+  T dx = px - k.cx[i];
+  T dy = py - k.cy[i];
+  return dx * dx + dy * dy - k.r2[i];
 }
 
 // h for W points at once (obstacle loop outer, points inner => W-wide ILP).
@@ -139,19 +151,46 @@ __device__ __forceinline__ T h_circle(const DSpec<T>& s, int i, T px, T py) {  /
 // spec to scratch and tripled the line-search cost.  h_grad (W = 1) is specialised below.
 constexpr int kFastObs = 8;
 
+template <typename T, int MO>
+__device__ __forceinline__ T h_smoothmin1(const DSpec<T>& s, T px, T py) {
+  T hm = h_circle(s, 0, px, py);
+#pragma unroll
+  for (int i = 1; i < MO; ++i) hm = m_min(hm, h_circle(s, i, px, py));
+  const T zmax = s.neg_beta * hm;
+  T se = T(0);
+#pragma unroll
+  for (int i = 0; i < MO; ++i) se += m_exp(s.neg_beta * h_circle(s, i, px, py) - zmax);
+  return s.neg_inv_beta * (zmax + m_log(se));
+}
+
 template <typename T, int W>
 __device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* py, T* h) {
-  if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0) {
-    T zmax[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) zmax[w] = s.neg_beta * h_circle(s, 0, px[w], py[w]);
-    for (int i = 1; i < s.M; ++i) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        T z = s.neg_beta * h_circle(s, i, px[w], py[w]);
-        zmax[w] = z > zmax[w] ? z : zmax[w];
+  if constexpr (W == 1) {
+    // single point (commit / rollout / plant): a dependent chain, so the compile-time count matters
+    if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0 && s.M <= kFastObs) {
+      switch (s.M) {  // wave-uniform
+        case 1: h[0] = h_smoothmin1<T, 1>(s, px[0], py[0]); return;
+        case 2: h[0] = h_smoothmin1<T, 2>(s, px[0], py[0]); return;
+        case 3: h[0] = h_smoothmin1<T, 3>(s, px[0], py[0]); return;
+        case 4: h[0] = h_smoothmin1<T, 4>(s, px[0], py[0]); return;
+        case 5: h[0] = h_smoothmin1<T, 5>(s, px[0], py[0]); return;
+        case 6: h[0] = h_smoothmin1<T, 6>(s, px[0], py[0]); return;
+        case 7: h[0] = h_smoothmin1<T, 7>(s, px[0], py[0]); return;
+        default: h[0] = h_smoothmin1<T, 8>(s, px[0], py[0]); return;
       }
     }
+  }
+  if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0) {
+    // max_i fl(-beta h_i) == fl(-beta min_i h_i) (rounding is monotone): one v_min per obstacle
+    T zmax[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) zmax[w] = h_circle(s, 0, px[w], py[w]);
+    for (int i = 1; i < s.M; ++i) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) zmax[w] = m_min(zmax[w], h_circle(s, i, px[w], py[w]));
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) zmax[w] = s.neg_beta * zmax[w];
     T se[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) se[w] = T(0);
@@ -201,8 +240,8 @@ __device__ __forceinline__ T h_grad_fixed(const DSpec<T>& s, T px, T py, T& gx, 
   for (int i = 0; i < MO; ++i) {
     T e = m_exp(z[i] - zmax);
     se += e;
-    sx += e * (T(2) * (px - s.cx[i]));
-    sy += e * (T(2) * (py - s.cy[i]));
+    sx += e * (T(2) * (px - kspec<T>().cx[i]));
+    sy += e * (T(2) * (py - kspec<T>().cy[i]));
   }
   T inv = m_rcp(se);
   gx = sx * inv;
@@ -234,8 +273,8 @@ __device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy)
     for (int i = 0; i < s.M; ++i) {
       T e = m_exp(s.neg_beta * h_circle(s, i, px, py) - zmax);
       se += e;
-      sx += e * (T(2) * (px - s.cx[i]));
-      sy += e * (T(2) * (py - s.cy[i]));
+      sx += e * (T(2) * (px - kspec<T>().cx[i]));
+      sy += e * (T(2) * (py - kspec<T>().cy[i]));
     }
     T inv = m_rcp(se);
     gx = sx * inv;
@@ -252,13 +291,13 @@ __device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy)
         am = i;
       }
     }
-    gx = T(2) * (px - s.cx[am]);
-    gy = T(2) * (py - s.cy[am]);
+    gx = T(2) * (px - kspec<T>().cx[am]);
+    gy = T(2) * (py - kspec<T>().cy[am]);
     return hm;
   }
   if (s.agg == DTMPC_OBS_SINGLE && s.M > 0) {
-    gx = T(2) * (px - s.cx[0]);
-    gy = T(2) * (py - s.cy[0]);
+    gx = T(2) * (px - kspec<T>().cx[0]);
+    gy = T(2) * (py - kspec<T>().cy[0]);
     return h_circle(s, 0, px, py);
   }
   gx = T(0);
