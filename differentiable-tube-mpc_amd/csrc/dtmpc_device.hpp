@@ -107,6 +107,14 @@ struct DIlqr {
   int max_iter, na;
   T tol, reg;
   T alphas[DTMPC_MAX_ALPHAS];
+  // line-search candidates that need a rollout: the non-zero alphas in order (calphas, original
+  // positions cpos), and zpos = position of the first alpha == 0 (-1 if none).  The alpha = 0
+  // candidate is clamp(V + 0 du) = V, i.e. the current tape, whose cost is the previous iteration's
+  // best J (or the initial tape's cost): it is never rolled out (core/ddp.py:256-301 semantics kept,
+  // including the first-wins tie order).
+  int nc, zpos;
+  int cpos[DTMPC_MAX_ALPHAS];
+  T calphas[DTMPC_MAX_ALPHAS];
 };
 
 // One trajectory's view of a SoA [rows][F][B] array: element (k, f) of lane `lane` lives at

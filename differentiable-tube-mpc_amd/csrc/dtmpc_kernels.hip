@@ -72,6 +72,25 @@ static DIlqr<T> make_ilqr(const dtmpc_ilqr_cfg& c) {
   o.tol = T(c.tol);
   o.reg = T(c.reg);
   for (int a = 0; a < DTMPC_MAX_ALPHAS; ++a) o.alphas[a] = T(c.alphas[a]);
+  o.zpos = -1;
+  o.nc = 0;
+  for (int a = 0; a < c.n_alphas; ++a) {
+    if (c.alphas[a] == 0.0) {
+      if (o.zpos < 0) o.zpos = a;
+    } else {
+      o.cpos[o.nc] = a;
+      o.calphas[o.nc] = T(c.alphas[a]);
+      ++o.nc;
+    }
+  }
+  if (o.nc == 0) {  // only zero alphas: roll them out like any other candidate
+    o.zpos = -1;
+    o.nc = c.n_alphas;
+    for (int a = 0; a < c.n_alphas; ++a) {
+      o.cpos[a] = a;
+      o.calphas[a] = T(c.alphas[a]);
+    }
+  }
   return o;
 }
 
@@ -511,7 +530,7 @@ static int launch_ilqr(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_i
   DSpec<T> s = make_spec<T>(*sp);
   DCost<T> c = make_cost<T>(*cp);
   DIlqr<T> cfg = make_ilqr<T>(*cf);
-  switch (cf->n_alphas) {
+  switch (cfg.nc) {  // rolled-out candidates (alpha = 0 is taken from the previous iteration)
 #define CASE(n) \
   case n: launch_ilqr_na<T, n>(s, c, cfg, (int)B, x0, Xref, Uref, X, U, K, kff, iters, status, st); break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
@@ -554,9 +573,8 @@ static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B
     a.wlo[f] = T(cf->w_low[f]);
     a.whi[f] = T(cf->w_high[f]);
   }
-  // the fused kernel runs both solves with one line-search width
-  int na = cf->nom_ilqr.n_alphas;
-  switch (na) {
+  // the fused kernel runs both solves with one line-search width (same alphas, checked)
+  switch (cfn.nc) {
 #define CASE(n)                                                                                     \
   case n:                                                                                           \
     hipLaunchKernelGGL((tube_step_kernel<T, n>), grid_for(B), dim3(kBlock), 0, st, s, cn, cfn, cfa, a); \

@@ -177,17 +177,19 @@ __device__ __forceinline__ void load_step(StepIn<T>& L, const DCost<T>& c, const
 }
 
 // ---------------------------------------------------------------------------------------------
-// line search (core/ddp.py:256-301): all NA candidates advance together; returns the index of the
-// strictly smallest cost (first wins ties) or -1 if any candidate is non-finite.
-template <typename T, int NA>
+// line search (core/ddp.py:256-301): the NC rolled-out candidates (cfg.calphas) advance together;
+// the alpha = 0 candidate (cfg.zpos) has cost Jprev (the current tape).  Returns the ORIGINAL index
+// of the strictly smallest cost (first wins ties), with its alpha in al_out, or -1 if any candidate is
+// non-finite.
+template <typename T, int NC>
 __device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg,
-                           const T* x0, T Bc0, const Col<T>& X, const Col<T>& U, const Col<T>& K,
-                           const Col<T>& kf, const Col<T>& Xr, int rf, const Col<T>& Ur,
-                           T& bestJ) {
+                                           const T* x0, T Bc0, const Col<T>& X, const Col<T>& U,
+                                           const Col<T>& K, const Col<T>& kf, const Col<T>& Xr, int rf,
+                                           const Col<T>& Ur, T Jprev, T& bestJ, T& al_out) {
   const int N = s.N;
-  T a0[NA], a1[NA], a2[NA], ab[NA], Bc[NA], J[NA];
+  T a0[NC], a1[NC], a2[NC], ab[NC], Bc[NC], J[NC];
 #pragma unroll
-  for (int a = 0; a < NA; ++a) {
+  for (int a = 0; a < NC; ++a) {
     a0[a] = x0[0];
     a1[a] = x0[1];
     a2[a] = x0[2];
@@ -204,40 +206,91 @@ __device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c,
 #pragma unroll
     for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
     if (k + kPrefetch < N) load_step(q[kPrefetch - 1], c, X, U, K, kf, Xr, rf, Ur, k + kPrefetch);
-    T u0[NA], u1[NA];
+    T u0[NC], u1[NC];
 #pragma unroll
-    for (int a = 0; a < NA; ++a) {
+    for (int a = 0; a < NC; ++a) {
       T e0 = a0[a] - cur.X0, e1 = a1[a] - cur.X1, e2 = a2[a] - cur.X2, e3 = ab[a] - cur.X3;
       T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
       T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
-      T al = cfg.alphas[a];
+      T al = cfg.calphas[a];
       u0[a] = clampv(cur.V0 + al * du0, s.umin0, s.umax0);
       u1[a] = clampv(cur.V1 + al * du1, s.umin1, s.umax1);
       J[a] = J[a] + stage_cost(c, a0[a], a1[a], a2[a], ab[a], u0[a], u1[a], cur.r0, cur.r1, cur.r2,
                                cur.q0, cur.q1);
     }
-    fhat_vec<T, NA>(s, a0, a1, a2, ab, u0, u1, Bc);
+    fhat_vec<T, NC>(s, a0, a1, a2, ab, u0, u1, Bc);
   }
   T r0, r1, r2;
   load_ref(c, Xr, rf, N, r0, r1, r2);
-  int best = 0;
   bool ok = true;
 #pragma unroll
-  for (int a = 0; a < NA; ++a) {
+  for (int a = 0; a < NC; ++a) {
     J[a] = J[a] + term_cost(c, a0[a], a1[a], a2[a], ab[a], r0, r1, r2);
     ok = ok && finite(J[a]);
   }
+  // first strict minimum among the rolled-out candidates (their relative order is the original one)
+  int bc = 0;
   bestJ = J[0];
 #pragma unroll
-  for (int a = 1; a < NA; ++a) {
+  for (int a = 1; a < NC; ++a) {
     if (J[a] < bestJ) {
       bestJ = J[a];
-      best = a;
+      bc = a;
     }
+  }
+  int best = cfg.cpos[0];
+  al_out = cfg.calphas[0];
+#pragma unroll
+  for (int a = 1; a < NC; ++a) {
+    if (bc == a) {
+      best = cfg.cpos[a];
+      al_out = cfg.calphas[a];
+    }
+  }
+  if (cfg.zpos >= 0) {
+    // the zero candidate sits at zpos: it wins iff it is strictly below every earlier candidate and
+    // not above any later one
+    T mb = T(0), ma = T(0);
+    bool hb = false, ha = false;
+#pragma unroll
+    for (int a = 0; a < NC; ++a) {
+      if (cfg.cpos[a] < cfg.zpos) {
+        mb = (!hb || J[a] < mb) ? J[a] : mb;
+        hb = true;
+      } else {
+        ma = (!ha || J[a] < ma) ? J[a] : ma;
+        ha = true;
+      }
+    }
+    if ((!hb || Jprev < mb) && (!ha || Jprev <= ma)) {
+      best = cfg.zpos;
+      bestJ = Jprev;
+      al_out = T(0);
+    }
+    ok = ok && finite(Jprev);
   }
   return ok ? best : -1;
 }
 
+// cost of the tape (X, U) with the line search's accumulation order: the alpha = 0 candidate's cost
+// before the first iteration (core/ddp.py:256-301 rolls it out; it is the initial tape)
+template <typename T>
+__device__ __forceinline__ T tape_cost(const DCost<T>& c, const Col<T>& X, const Col<T>& U,
+                                       const Col<T>& Xr, int rf, const Col<T>& Ur, int N) {
+  T J = T(0);
+  for (int k = 0; k < N; ++k) {
+    T r0, r1, r2, q0, q1;
+    load_ref(c, Xr, rf, k, r0, r1, r2);
+    load_uref(c, Ur, k, q0, q1);
+    J = J + stage_cost(c, X.at(k, 4, 0), X.at(k, 4, 1), X.at(k, 4, 2), X.at(k, 4, 3), U.at(k, 2, 0),
+                       U.at(k, 2, 1), r0, r1, r2, q0, q1);
+  }
+  T r0, r1, r2;
+  load_ref(c, Xr, rf, N, r0, r1, r2);
+  return J + term_cost(c, X.at(N, 4, 0), X.at(N, 4, 1), X.at(N, 4, 2), X.at(N, 4, 3), r0, r1, r2);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Materialise the chosen candidate in place: X, U <- rollout with step alpha (same arithmetic
 // as the candidate lane of line_search).  X[k+1] of the old tape is read before it is replaced.
 template <typename T>
@@ -309,6 +362,8 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
   }
   rollout_traj(s, x0, X, U);
   T Bc0 = barrier_of_state(s, x0[0], x0[1]);
+  // cost of the current tape = the alpha = 0 candidate's cost (only needed when alpha = 0 is listed)
+  T Jcur = cfg.zpos >= 0 && cfg.max_iter > 0 ? tape_cost(c, X, U, Xr, rf, Ur, N) : T(0);
   pr.mark(pb + 0);
   bool have_prev = false;
   T prev = T(0);
@@ -317,12 +372,12 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
     iters = it + 1;
     if (!ilqr_backward(s, c, cfg.reg, X, U, K, kf, Xr, rf, Ur)) return DTMPC_ST_NONFINITE;
     pr.mark(pb + 1);
-    T bestJ;
-    int best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, K, kf, Xr, rf, Ur, bestJ);
+    T bestJ, al;
+    int best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, K, kf, Xr, rf, Ur, Jcur, bestJ, al);
     pr.mark(pb + 2);
     if (best < 0) return DTMPC_ST_NONFINITE;
-    T al = cfg.alphas[best];
     if (al != T(0)) commit_candidate(s, al, x0, Bc0, X, U, K, kf);
+    Jcur = bestJ;
     pr.mark(pb + 3);
     // :303-305
     if (have_prev && m_abs(prev - bestJ) < cfg.tol) break;
