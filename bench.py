@@ -67,7 +67,7 @@ def pmc_traffic(batch: int):
     """Per-launch HBM bytes of tube_step_kernel from a committed rocprofv3 --pmc summary (or None).
     FETCH_SIZE is doubled (gfx950 under-reports wide coalesced reads by 2x, MI355X_MICROARCH.md §HBM)."""
     best = None
-    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json"))):
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True)):
         try:
             d = json.load(open(p))
         except Exception:
