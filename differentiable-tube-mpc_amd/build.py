@@ -1,6 +1,7 @@
 """Build libdtmpc.so (HIP, gfx950) in-tree: differentiable-tube-mpc_amd/diff_tube_mpc_strict_pt/libdtmpc.so.
 
-Plain hipcc, no build system: one translation unit (csrc/dtmpc_kernels.hip).
+Plain hipcc, no build system: two translation units (csrc/dtmpc_kernels.hip: paper path + per-function
+entry points; csrc/dtmpc_general.hip: general IFT path) compiled in parallel, then linked.
 """
 from __future__ import annotations
 
@@ -9,21 +10,22 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "dtmpc_kernels.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solver.hpp")] + [
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_kernels.hip", "dtmpc_general.hip")]
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solver.hpp", "dtmpc_general.hpp",
+                                                 "dtmpc_host.hpp")] + [
     os.path.join(os.path.dirname(HERE), "include", "dtmpc.h")
 ]
 OUT = os.path.join(HERE, "diff_tube_mpc_strict_pt", "libdtmpc.so")
 ARCH = os.environ.get("DTMPC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17", "-Wall", "-Wno-unused-function"]
+FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
 
 
 def up_to_date() -> bool:
     if not os.path.exists(OUT):
         return False
     t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(p) <= t for p in [SRC, *DEPS, __file__])
+    return all(os.path.getmtime(p) <= t for p in [*SRCS, *DEPS, __file__])
 
 
 def build(force: bool = False, variant: str = "", defines=()) -> str:
@@ -33,9 +35,21 @@ def build(force: bool = False, variant: str = "", defines=()) -> str:
     out = OUT if not variant else OUT.replace("libdtmpc.so", f"libdtmpc_{variant}.so")
     if not variant and not force and up_to_date():
         return out
-    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-o", out + ".tmp", SRC]
+    objs = []
+    procs = []
+    for src in SRCS:
+        obj = out + "." + os.path.splitext(os.path.basename(src))[0] + ".o"
+        cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-c", "-o", obj, src]
+        print("[build]", " ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    if any([p.wait() != 0 for p in procs]):
+        raise subprocess.CalledProcessError(1, "hipcc")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(out + ".tmp", out)
     return out
 

@@ -93,6 +93,7 @@ struct DSpec {
   T dt, umin0, umin1, umax0, umax1, active_tol;
   T neg_beta, neg_inv_beta;  // (-beta), -(1/beta) as the reference's python floats
   T alpha, gamma, eps;
+  T tight;  // h offset of the DBaS dynamics (nominal tightening s, core/tube_mpc.py:151-153); 0 else
   T cx[DTMPC_MAX_OBS], cy[DTMPC_MAX_OBS], r2[DTMPC_MAX_OBS];
 };
 
@@ -356,6 +357,7 @@ __device__ __forceinline__ T barrier_dyn(const DSpec<T>& s, T z) {
 // dynamics: W DBaS-augmented Dubins steps at once.
 //   x' = dubins_step(x, u)            core/systems/dubins.py:26-45
 //   b' = B(h(x')) - gamma (B(h(x)) - b) core/barrier.py:75-108
+// With a tightened nominal h_nom = h - s enters the barrier (core/tube_mpc.py:235-238; s = 0 else).
 // Bc[w] carries B(h(x_k)) from the previous step (the reference recomputes h(x_k) inside
 // dbas_step; the value is the same function of the same state), and is updated to B(h(x_{k+1})).
 template <typename T, int W>
@@ -374,7 +376,7 @@ __device__ __forceinline__ void fhat_vec(const DSpec<T>& s, T* x0, T* x1, T* x2,
   h_vec<T, W>(s, x0, x1, hn);
 #pragma unroll
   for (int w = 0; w < W; ++w) {
-    T Bn = barrier_dyn(s, hn[w]);
+    T Bn = barrier_dyn(s, hn[w] - s.tight);
     b[w] = Bn - s.gamma * (Bc[w] - b[w]);
     Bc[w] = Bn;
   }
@@ -384,7 +386,7 @@ template <typename T>
 __device__ __forceinline__ T barrier_of_state(const DSpec<T>& s, T px, T py) {
   T h[1], x[1] = {px}, y[1] = {py};
   h_vec<T, 1>(s, x, y, h);
-  return barrier_dyn(s, h[0]);
+  return barrier_dyn(s, h[0] - s.tight);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -632,6 +634,14 @@ __device__ __forceinline__ bool riccati_step(const Jac<T>& J, const T* lx, const
       R.Vxx[i][j] = Qxx[i][j] + m1 + M2[i][j] + M2[j][i];
     }
   return ok;
+}
+
+// fixed-order wave64 sum (lane 0 holds the result)
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,0 +1,162 @@
+// dtmpc_host.hpp — host-side helpers shared by the translation units of libdtmpc.so:
+// C struct -> typed device descriptor conversion, argument checks, launch error reporting.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/dtmpc.h"
+#include "dtmpc_general.hpp"
+
+namespace dtmpc {
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------------------------------------
+// host-side conversion of the C structs into the typed device descriptors
+template <typename T>
+inline DSpec<T> make_spec(const dtmpc_spec& p) {
+  DSpec<T> s;
+  std::memset(&s, 0, sizeof(s));
+  s.N = p.horizon;
+  s.M = p.n_obstacles;
+  s.agg = p.obs_aggregation;
+  s.barrier = p.barrier_type;
+  s.dt = T(p.dt);
+  s.umin0 = T(p.u_min[0]);
+  s.umin1 = T(p.u_min[1]);
+  s.umax0 = T(p.u_max[0]);
+  s.umax1 = T(p.u_max[1]);
+  s.active_tol = T(p.active_tol);
+  s.neg_beta = T(-p.obs_beta);
+  s.neg_inv_beta = T(-(1.0 / p.obs_beta));
+  s.alpha = T(p.dbas_alpha);
+  s.gamma = T(p.dbas_gamma);
+  s.eps = T(p.dbas_eps);
+  s.tight = T(p.h_offset);
+  for (int i = 0; i < p.n_obstacles && i < DTMPC_MAX_OBS; ++i) {
+    s.cx[i] = T(p.obs_cx[i]);
+    s.cy[i] = T(p.obs_cy[i]);
+    s.r2[i] = T(p.obs_r[i] * p.obs_r[i]);
+  }
+  return s;
+}
+
+template <typename T>
+inline DCost<T> make_cost(const dtmpc_cost& c) {
+  DCost<T> o;
+  o.kind = c.kind;
+  o.wrap = c.wrap_angle;
+  o.Q0 = T(c.Q[0]);
+  o.Q1 = T(c.Q[1]);
+  o.Q2 = T(c.Q[2]);
+  o.R0 = T(c.R[0]);
+  o.R1 = T(c.R[1]);
+  o.Qf0 = T(c.Qf[0]);
+  o.Qf1 = T(c.Qf[1]);
+  o.Qf2 = T(c.Qf[2]);
+  o.qb = T(c.qb);
+  o.t0 = T(c.target[0]);
+  o.t1 = T(c.target[1]);
+  o.t2 = T(c.target[2]);
+  return o;
+}
+
+template <typename T>
+inline DIlqr<T> make_ilqr(const dtmpc_ilqr_cfg& c) {
+  DIlqr<T> o;
+  std::memset(&o, 0, sizeof(o));
+  o.max_iter = c.max_iter;
+  o.na = c.n_alphas;
+  o.tol = T(c.tol);
+  o.reg = T(c.reg);
+  for (int a = 0; a < DTMPC_MAX_ALPHAS; ++a) o.alphas[a] = T(c.alphas[a]);
+  o.zpos = -1;
+  o.nc = 0;
+  for (int a = 0; a < c.n_alphas; ++a) {
+    if (c.alphas[a] == 0.0) {
+      if (o.zpos < 0) o.zpos = a;
+    } else {
+      o.cpos[o.nc] = a;
+      o.calphas[o.nc] = T(c.alphas[a]);
+      ++o.nc;
+    }
+  }
+  if (o.nc == 0) {  // only zero alphas: roll them out like any other candidate
+    o.zpos = -1;
+    o.nc = c.n_alphas;
+    for (int a = 0; a < c.n_alphas; ++a) {
+      o.cpos[a] = a;
+      o.calphas[a] = T(c.alphas[a]);
+    }
+  }
+  return o;
+}
+
+template <typename T>
+__device__ __forceinline__ Col<T> col(void* p, int64_t i, int B) {
+  Col<T> c;
+  c.base = reinterpret_cast<T*>(p);
+  c.ld = (unsigned)B;
+  c.lane = (unsigned)i;
+  return c;
+}
+template <typename T>
+__device__ __forceinline__ Col<T> col(const void* p, int64_t i, int B) {
+  return col<T>(const_cast<void*>(p), i, B);
+}
+
+// last-error text, shared by every translation unit of libdtmpc.so (inline function static)
+inline char* err_buf() {
+  static thread_local char buf[512] = "";
+  return buf;
+}
+
+inline int set_err(int code, const char* msg) {
+  std::snprintf(err_buf(), 512, "%s", msg);
+  return code;
+}
+
+inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    std::snprintf(err_buf(), 512, "%s: %s", what, hipGetErrorString(e));
+    return DTMPC_ERR_HIP;
+  }
+  return DTMPC_OK;
+}
+
+inline int check_spec(const dtmpc_spec* s, int64_t B) {
+  if (!s) return set_err(DTMPC_ERR_BAD_ARG, "spec is NULL");
+  if (s->horizon < 1 || s->horizon > DTMPC_MAX_HORIZON) return set_err(DTMPC_ERR_BAD_ARG, "horizon out of range");
+  if (s->n_obstacles < 0 || s->n_obstacles > DTMPC_MAX_OBS) return set_err(DTMPC_ERR_BAD_ARG, "n_obstacles out of range");
+  if (s->obs_aggregation < 0 || s->obs_aggregation > DTMPC_OBS_NONE) return set_err(DTMPC_ERR_BAD_ARG, "bad obs_aggregation");
+  if (s->barrier_type != DTMPC_BARRIER_INVERSE && s->barrier_type != DTMPC_BARRIER_LOG) return set_err(DTMPC_ERR_BAD_ARG, "bad barrier_type");
+  if (s->dbas_alpha < 0) return set_err(DTMPC_ERR_BAD_ARG, "alpha must be >= 0");
+  if (!(s->dbas_gamma >= -1.0 && s->dbas_gamma <= 1.0)) return set_err(DTMPC_ERR_BAD_ARG, "gamma must be in [-1, 1]");
+  if (s->obs_aggregation == DTMPC_OBS_SMOOTHMIN && !(s->obs_beta > 0)) return set_err(DTMPC_ERR_BAD_ARG, "obs_beta must be > 0");
+  if (B < 1) return set_err(DTMPC_ERR_BAD_ARG, "batch must be >= 1");
+  // 32-bit in-kernel offsets: (rows * fields) * B must fit
+  if ((int64_t)(s->horizon + 1) * 20 * B >= (int64_t)1 << 31) return set_err(DTMPC_ERR_BAD_ARG, "batch too large for 32-bit tape offsets");
+  return DTMPC_OK;
+}
+
+inline int check_ilqr(const dtmpc_ilqr_cfg* c) {
+  if (!c) return set_err(DTMPC_ERR_BAD_ARG, "ilqr cfg is NULL");
+  if (c->n_alphas < 1 || c->n_alphas > DTMPC_MAX_ALPHAS) return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
+  if (c->max_iter < 0) return set_err(DTMPC_ERR_BAD_ARG, "max_iter must be >= 0");
+  return DTMPC_OK;
+}
+
+inline int check_cost(const dtmpc_cost* c, const void* Xref, const void* Uref) {
+  if (!c) return set_err(DTMPC_ERR_BAD_ARG, "cost is NULL");
+  if (c->kind != DTMPC_COST_TARGET && c->kind != DTMPC_COST_TRACK) return set_err(DTMPC_ERR_BAD_ARG, "bad cost kind");
+  if (c->kind == DTMPC_COST_TRACK && (!Xref || !Uref)) return set_err(DTMPC_ERR_BAD_ARG, "tracking cost needs Xref and Uref");
+  return DTMPC_OK;
+}
+
+inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + kBlock - 1) / kBlock)); }
+
+}  // namespace dtmpc

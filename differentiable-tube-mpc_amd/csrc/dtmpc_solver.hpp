@@ -388,6 +388,51 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
 }
 
 // ---------------------------------------------------------------------------------------------
+// Q-blocks of the sensitivity backward step (core/ddp.py:374-377) with l_ux = 0:
+//   Q_xx = l_xx + A^T V_xx A, Q_xu = A^T V_xx B, Q_ux = B^T V_xx A, Q_uu = l_uu + B^T V_xx B
+template <typename T>
+__device__ __forceinline__ void sens_qblocks(const Jac<T>& J, const T (&V)[4][4], const T* lxx, const T* luu,
+                                             T (&Qxx)[4][4], T (&Qxu)[4][2], T (&Qux)[2][4],
+                                             T (&Quu)[2][2]) {
+  T P[4][4];  // A^T V_xx
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    P[0][j] = V[0][j] + J.a30 * V[3][j];
+    P[1][j] = V[1][j] + J.a31 * V[3][j];
+    P[2][j] = J.a02 * V[0][j] + J.a12 * V[1][j] + V[2][j] + J.a32 * V[3][j];
+    P[3][j] = J.g * V[3][j];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    Qxx[i][0] = P[i][0] + P[i][3] * J.a30;
+    Qxx[i][1] = P[i][1] + P[i][3] * J.a31;
+    Qxx[i][2] = P[i][0] * J.a02 + P[i][1] * J.a12 + P[i][2] + P[i][3] * J.a32;
+    Qxx[i][3] = P[i][3] * J.g;
+    Qxx[i][i] = lxx[i] + Qxx[i][i];
+    // Q_xu = l_ux^T + A^T V_xx B   (:380)
+    Qxu[i][0] = P[i][0] * J.b00 + P[i][1] * J.b10 + P[i][3] * J.b30;
+    Qxu[i][1] = P[i][2] * J.b21 + P[i][3] * J.b31;
+  }
+  T S[2][4];  // B^T V_xx
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    S[0][j] = J.b00 * V[0][j] + J.b10 * V[1][j] + J.b30 * V[3][j];
+    S[1][j] = J.b21 * V[2][j] + J.b31 * V[3][j];
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    Qux[a][0] = S[a][0] + S[a][3] * J.a30;
+    Qux[a][1] = S[a][1] + S[a][3] * J.a31;
+    Qux[a][2] = S[a][0] * J.a02 + S[a][1] * J.a12 + S[a][2] + S[a][3] * J.a32;
+    Qux[a][3] = S[a][3] * J.g;
+    Quu[a][0] = S[a][0] * J.b00 + S[a][1] * J.b10 + S[a][3] * J.b30;
+    Quu[a][1] = S[a][2] * J.b21 + S[a][3] * J.b31;
+  }
+  Quu[0][0] = luu[0] + Quu[0][0];
+  Quu[1][1] = luu[1] + Quu[1][1];
+}
+
+// ---------------------------------------------------------------------------------------------
 // DDP sensitivity (core/ddp.py:317-427) with the paper upper loss (core/tube_mpc.py:932-944):
 //   g_x(k) = [2 (x_k - xbar_k), 2 b_k], g_u = 0, same at k = N.
 // AB scratch [N][10]: a02 a12 a30 a31 a32 b00 b10 b30 b31 act(=act0 + 2 act1).
@@ -436,45 +481,8 @@ __device__ __forceinline__ int sens_traj(const DSpec<T>& s, const DCost<T>& c, c
     gxn = gxk;
     gyn = gyk;
     dBn = dBk;
-    const T(&V)[4][4] = R.Vxx;
-    T P[4][4];  // A^T V_xx
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      P[0][j] = V[0][j] + J.a30 * V[3][j];
-      P[1][j] = V[1][j] + J.a31 * V[3][j];
-      P[2][j] = J.a02 * V[0][j] + J.a12 * V[1][j] + V[2][j] + J.a32 * V[3][j];
-      P[3][j] = J.g * V[3][j];
-    }
-    T Qxx[4][4], Qxu[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      Qxx[i][0] = P[i][0] + P[i][3] * J.a30;
-      Qxx[i][1] = P[i][1] + P[i][3] * J.a31;
-      Qxx[i][2] = P[i][0] * J.a02 + P[i][1] * J.a12 + P[i][2] + P[i][3] * J.a32;
-      Qxx[i][3] = P[i][3] * J.g;
-      Qxx[i][i] = lxx[i] + Qxx[i][i];
-      // Q_xu = l_ux^T + A^T V_xx B   (:380)
-      Qxu[i][0] = P[i][0] * J.b00 + P[i][1] * J.b10 + P[i][3] * J.b30;
-      Qxu[i][1] = P[i][2] * J.b21 + P[i][3] * J.b31;
-    }
-    T S[2][4];  // B^T V_xx
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      S[0][j] = J.b00 * V[0][j] + J.b10 * V[1][j] + J.b30 * V[3][j];
-      S[1][j] = J.b21 * V[2][j] + J.b31 * V[3][j];
-    }
-    T Qux[2][4], Quu[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      Qux[a][0] = S[a][0] + S[a][3] * J.a30;
-      Qux[a][1] = S[a][1] + S[a][3] * J.a31;
-      Qux[a][2] = S[a][0] * J.a02 + S[a][1] * J.a12 + S[a][2] + S[a][3] * J.a32;
-      Qux[a][3] = S[a][3] * J.g;
-      Quu[a][0] = S[a][0] * J.b00 + S[a][1] * J.b10 + S[a][3] * J.b30;
-      Quu[a][1] = S[a][2] * J.b21 + S[a][3] * J.b31;
-    }
-    Quu[0][0] = luu[0] + Quu[0][0];
-    Quu[1][1] = luu[1] + Quu[1][1];
+    T Qxx[4][4], Qxu[4][2], Qux[2][4], Quu[2][2];
+    sens_qblocks(J, R.Vxx, lxx, luu, Qxx, Qxu, Qux, Quu);
     const T* tv = R.Vx;
     T tQu0 = J.b00 * tv[0] + J.b10 * tv[1] + J.b30 * tv[3];
     T tQu1 = J.b21 * tv[2] + J.b31 * tv[3];

@@ -7,11 +7,15 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_OBS = 16
 MAX_ALPHAS = 8
 MAX_HORIZON = 512
 LOG_FIELDS = 18
+GEN_LOG_FIELDS = 12
+GEN_SUMS = 24
+# raw parameter layout of the general path (include/dtmpc.h DTMPC_P_*)
+P_Q, P_R, P_QF, P_QB, P_ALPHA, P_GAMMA, P_TIGHT, P_COUNT = 0, 3, 5, 8, 9, 10, 11, 12
 
 F32, F64 = 0, 1
 OBS_SMOOTHMIN, OBS_MIN, OBS_SINGLE, OBS_NONE = 0, 1, 2, 3
@@ -41,6 +45,7 @@ class DtmpcSpec(C.Structure):
         ("dbas_alpha", C.c_double),
         ("dbas_gamma", C.c_double),
         ("dbas_eps", C.c_double),
+        ("h_offset", C.c_double),
     ]
 
 
@@ -109,6 +114,48 @@ class DtmpcTubeState(C.Structure):
     ]
 
 
+class DtmpcGeneralCfg(C.Structure):
+    _fields_ = [
+        ("target", C.c_double * 3),
+        ("nom_ilqr", DtmpcIlqrCfg),
+        ("aux_ilqr", DtmpcIlqrCfg),
+        ("adapt_nominal", C.c_int32),
+        ("adapt_ancillary", C.c_int32),
+        ("project_params", C.c_int32),
+        ("disturbance", C.c_int32),
+        ("write_log", C.c_int32),
+        ("pad_", C.c_int32),
+        ("seed", C.c_uint64),
+        ("w_low", C.c_double * 3),
+        ("w_high", C.c_double * 3),
+        ("lr_eta", C.c_double),
+        ("momentum", C.c_double),
+        ("clip_norm", C.c_double),
+    ]
+
+
+class DtmpcGeneralState(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p),
+        ("b", C.c_void_p),
+        ("xbar", C.c_void_p),
+        ("bbar", C.c_void_p),
+        ("Xnom", C.c_void_p),
+        ("Unom", C.c_void_p),
+        ("Xaux", C.c_void_p),
+        ("Uaux", C.c_void_p),
+        ("work", C.c_void_p),
+        ("theta", C.c_void_p),
+        ("velocity", C.c_void_p),
+        ("partials", C.c_void_p),
+        ("sums", C.c_void_p),
+        ("gout", C.c_void_p),
+        ("log", C.c_void_p),
+        ("status", C.c_void_p),
+        ("iters", C.c_void_p),
+    ]
+
+
 # Exported symbols and their ctypes prototypes: (restype, argtypes).  Both the loader and the
 # "library exports every declared symbol" test read this table.
 P = C.c_void_p
@@ -139,6 +186,26 @@ PROTOTYPES = {
     ),
     "dtmpc_partials_reduce": (C.c_int, [C.c_int, I64, P, P, P]),
     "dtmpc_theta_update": (C.c_int, [C.c_int, C.POINTER(DtmpcAdaptCfg), C.c_double, P, P, P, P]),
+    "dtmpc_sensitivity_upper_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64]),
+    "dtmpc_ddp_sensitivity_upper": (
+        C.c_int,
+        [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), I64, P, P, P, P, P, P, P, P, P, P],
+    ),
+    "dtmpc_ift_gradient": (
+        C.c_int,
+        [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(C.c_double), I64, P, P, P, P, P, P, P, P, P,
+         P, P],
+    ),
+    "dtmpc_general_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64]),
+    "dtmpc_general_step": (
+        C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcGeneralCfg), I64, C.POINTER(DtmpcGeneralState), P]),
+    "dtmpc_partials_reduce_n": (C.c_int, [C.c_int, I64, I32, P, P, P]),
+    "dtmpc_general_update": (
+        C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcGeneralCfg), C.c_double,
+                  C.POINTER(DtmpcGeneralState), P]),
+    "dtmpc_general_plant": (
+        C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcGeneralCfg), I64, I64, I64,
+                  C.POINTER(DtmpcGeneralState), P, P]),
 }
 
 

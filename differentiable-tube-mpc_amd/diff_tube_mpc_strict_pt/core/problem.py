@@ -271,3 +271,103 @@ def tracking_cost(theta: Sequence[float]) -> QuadraticCost:
     (core/tube_mpc.py:875-894)."""
     Q = tuple(float(v) for v in theta[:3])
     return QuadraticCost(kind="track", Q=Q, R=(float(theta[3]), float(theta[4])), Qf=Q, qb=float(theta[5]))
+
+
+# ---------------------------------------------------------------------------------------------
+# general (softplus / tanh parameterised) path, core/tube_mpc.py:40-663
+
+@dataclass(frozen=True)
+class GeneralSetup:
+    """Everything core/tube_mpc.py:48-188 derives from the config on the general path.
+
+    theta0 is the [2][12] raw parameter block of include/dtmpc.h (DTMPC_P_* layout): row 0 the
+    ancillary AuxiliaryTheta (Q, R, Qf, q_b, alpha, gamma; tight slot unused), row 1 the nominal
+    NominalTheta (+ tight).  Both start from cost_nominal's raw weights (:111-131; the ancillary
+    q_b from cost_auxiliary.q_b when given) and the DBaS alpha / gamma / nominal_tightening."""
+
+    problem: DubinsDBaSProblem        # system + obstacles + barrier type + eps (alpha/gamma from theta)
+    target: Tuple[float, float, float]
+    theta0: Tuple[Tuple[float, ...], Tuple[float, ...]]
+    ilqr_nom: ILQRConfig
+    ilqr_aux: ILQRConfig
+    adapt_nominal: bool
+    adapt_ancillary: bool
+    lr_eta: float
+    momentum: float
+    clip_norm: float
+    project_params: bool
+    w_low: Tuple[float, float, float]
+    w_high: Tuple[float, float, float]
+    x0: Tuple[float, float, float] = (0.0, 0.0, math.pi / 4)
+    use_float64: bool = False
+    task_horizon: int = 300
+    adapt_steps: int = 1
+
+    def to_c(self, *, disturbance: int = 0, seed: int = 0, write_log: bool = False) -> _abi.DtmpcGeneralCfg:
+        c = _abi.DtmpcGeneralCfg()
+        for i in range(3):
+            c.target[i] = float(self.target[i])
+            c.w_low[i] = float(self.w_low[i])
+            c.w_high[i] = float(self.w_high[i])
+        c.nom_ilqr = self.ilqr_nom.to_c()
+        c.aux_ilqr = self.ilqr_aux.to_c()
+        c.adapt_nominal = 1 if self.adapt_nominal else 0
+        c.adapt_ancillary = 1 if self.adapt_ancillary else 0
+        c.project_params = 1 if self.project_params else 0
+        c.disturbance = int(disturbance)
+        c.write_log = 1 if write_log else 0
+        c.seed = int(seed) & ((1 << 64) - 1)
+        c.lr_eta = float(self.lr_eta)
+        c.momentum = float(self.momentum)
+        c.clip_norm = float(self.clip_norm)
+        return c
+
+
+def general_setup_from_config(cfg: Dict[str, Any]) -> GeneralSetup:
+    """General-path wiring of core/tube_mpc.py:48-188."""
+    sc = cfg["system"]
+    env = cfg.get("environment", {})
+    if "obstacles" not in env and "obstacle" not in env:
+        # the reference mixes h = 1 in the dynamics with a (5, 5, 1.5) circle in the Jacobian here
+        # (core/tube_mpc.py:82-84); that combination has no typed equivalent
+        raise NotImplementedError("the general path needs an obstacle set ('obstacles' or 'obstacle')")
+    problem = problem_from_config(cfg, alpha=0.0, gamma=0.0)
+    db = cfg["dbas"]
+    cn = cfg["cost_nominal"]
+    Q0 = tuple(float(v) for v in cn["Q"])
+    R0 = tuple(float(v) for v in cn["R"])
+    Qf0 = tuple(float(v) for v in cn["Qf"])
+    qb0 = float(cn["q_b"])
+    qb_aux0 = float(cfg.get("cost_auxiliary", {}).get("q_b", qb0))
+    a0, g0, s0 = float(db["alpha"]), float(db["gamma"]), float(db.get("nominal_tightening", 0.0))
+    aux = Q0 + R0 + Qf0 + (qb_aux0, a0, g0, 0.0)
+    nom = Q0 + R0 + Qf0 + (qb0, a0, g0, s0)
+    ad = cfg.get("adaptation", {})
+    N = int(sc["horizon_N"])
+    reg = float(sc.get("ilqr_reg", 1e-6))
+    dist = sc.get("disturbance", {})
+    return GeneralSetup(
+        problem=problem,
+        target=tuple(float(v) for v in sc["target"]),
+        theta0=(aux, nom),
+        # ILQRConfig(horizon, nx, nu, max_iter, reg): tol and line-search alphas keep the dataclass
+        # defaults (core/tube_mpc.py:161-162, core/ddp.py:12-20)
+        ilqr_nom=ILQRConfig(horizon=N, max_iter=int(sc.get("nominal_max_iter", 10)), reg=reg),
+        ilqr_aux=ILQRConfig(horizon=N, max_iter=int(sc.get("aux_max_iter", 10)), reg=reg),
+        adapt_nominal=bool(ad.get("adapt_nominal", True)),
+        adapt_ancillary=bool(ad.get("adapt_ancillary", True)),
+        lr_eta=float(ad.get("lr_eta", 1e-3)),
+        momentum=float(ad.get("momentum", 0.0)),
+        clip_norm=float(ad.get("grad_clip_norm", 0.0)),
+        project_params=bool(ad.get("project_params", False)),
+        w_low=tuple(float(v) for v in dist.get("w_low", (-0.05, -0.05, -0.05))),
+        w_high=tuple(float(v) for v in dist.get("w_high", (0.05, 0.05, 0.05))),
+        use_float64=bool(cfg.get("use_float64", False)),
+        task_horizon=int(sc.get("task_horizon_H", 300)),
+        adapt_steps=int(ad.get("steps", 1)),
+    )
+
+
+def softplus(x: float) -> float:
+    """torch.nn.functional.softplus (beta 1, threshold 20), core/params.py:9-11"""
+    return x if x > 20.0 else math.log1p(math.exp(x))

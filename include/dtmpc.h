@@ -33,11 +33,13 @@
 extern "C" {
 #endif
 
-#define DTMPC_ABI_VERSION 1
+#define DTMPC_ABI_VERSION 2
 #define DTMPC_MAX_OBS 16
 #define DTMPC_MAX_ALPHAS 8
 #define DTMPC_MAX_HORIZON 512
 #define DTMPC_LOG_FIELDS 18 /* rows of dtmpc_tube_state.log */
+#define DTMPC_GEN_LOG_FIELDS 12 /* rows of dtmpc_general_state.log */
+#define DTMPC_GEN_SUMS 24 /* L, ancillary raw-theta grads (11), nominal raw-theta-bar grads (12) */
 
 /* scalar type of the arrays */
 enum { DTMPC_F32 = 0, DTMPC_F64 = 1 };
@@ -91,6 +93,10 @@ typedef struct dtmpc_spec {
   double dbas_alpha;        /* DBaSConfig.alpha (core/barrier.py:29) */
   double dbas_gamma;        /* DBaSConfig.gamma, in [-1, 1] */
   double dbas_eps;          /* DBaSConfig.eps */
+  double h_offset;          /* constraint tightening s of the nominal MPC: the DBaS dynamics use
+                               h(x) - s (core/tube_mpc.py:151-153, 232-238); the linearisation
+                               differentiates the untightened h (core/tube_mpc.py:282-286).  0 for
+                               every other caller. */
 } dtmpc_spec;
 
 /* Quadratic stage/terminal cost (core/cost_derivs.py:58-146 + caller overrides in
@@ -244,6 +250,122 @@ int dtmpc_partials_reduce(int dtype, int64_t n_partials, const void* partials, v
  * the batch-mean gradient g = sums[1:7] * inv_batch.  theta [6] and velocity [6] in/out. */
 int dtmpc_theta_update(int dtype, const dtmpc_adapt_cfg* cfg, double inv_batch, const void* sums,
                        void* theta, void* velocity, void* stream);
+
+
+/* ---- general (softplus / tanh parameterised) IFT path ------------------------------------ */
+/*
+ * core/tube_mpc.py:40-663 with adapt_nominal (or paper_dubins_mode off): every weight and DBaS
+ * parameter is a raw, unconstrained value mapped through core/params.py:9-59 --
+ * Q = softplus(Q_raw), R, Qf, q_b likewise, alpha = softplus(alpha_raw) + 1e-6,
+ * gamma = tanh(gamma_raw), tightening s = softplus(tight_raw) -- and both the ancillary theta and
+ * the nominal theta-bar adapt by the IFT gradient (core/ift.py:35-92), the nominal one through the
+ * ancillary's gradient w.r.t. its reference trajectory (core/tube_mpc.py:509-584).
+ *
+ * Raw parameter vector layout ([12] per parameter set): */
+enum {
+  DTMPC_P_Q = 0,      /* Q_raw[3] */
+  DTMPC_P_R = 3,      /* R_raw[2] */
+  DTMPC_P_QF = 5,     /* Qf_raw[3] */
+  DTMPC_P_QB = 8,     /* qb_raw */
+  DTMPC_P_ALPHA = 9,  /* alpha_raw */
+  DTMPC_P_GAMMA = 10, /* gamma_raw */
+  DTMPC_P_TIGHT = 11, /* tight_raw (nominal theta-bar only; ignored for the ancillary set) */
+  DTMPC_P_COUNT = 12
+};
+
+/* Scratch bytes for dtmpc_ddp_sensitivity_upper. */
+size_t dtmpc_sensitivity_upper_workspace_bytes(int dtype, int32_t horizon, int64_t B);
+
+/* DDP-structured KKT sensitivity with ARBITRARY upper-level gradients:
+ *   replaces core/ddp.py:317-427 `ddp_sensitivity` with upper_grad_x / upper_grad_u /
+ *   upper_grad_xN given as arrays (the nominal solve of core/tube_mpc.py:523-554 feeds
+ *   [dL/dX_ref, 0] and dL/dU_ref from the ancillary IFT).
+ *   gX [N+1][4][B] (row N = upper_grad_xN), gU [N][2][B]; dX [N+1][4][B], dU [N][2][B],
+ *   dlam [N+1][4][B] (NULL skips delta_lambda). */
+int dtmpc_ddp_sensitivity_upper(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, int64_t B,
+                                const void* X, const void* U, const void* gX, const void* gU,
+                                void* dX, void* dU, void* dlam, void* work, int32_t* status,
+                                void* stream);
+
+/* IFT gradient w.r.t. the raw parameters, in closed form:
+ *   replaces core/ift.py:35-92 `ift_gradient` for the typed problem, with the closures of
+ *   core/tube_mpc.py:461-500 (cost->kind = DTMPC_COST_TRACK: ancillary, also dL/dX_ref, dL/dU_ref)
+ *   or :556-585 (DTMPC_COST_TARGET: nominal, with the tightening).  The weights and DBaS
+ *   parameters are taken from theta_raw (host [12]) through core/params.py, not from cost/spec;
+ *   cost supplies kind and target, spec the system, obstacles, barrier type and eps.
+ *   X, U, dX, dU, dlam: optimum and its sensitivity (dtmpc_ddp_sensitivity*).
+ *   g_theta [12][B] out (row DTMPC_P_TIGHT is 0 for the ancillary), g_xref [N+1][3][B] and
+ *   g_uref [N][2][B] out for DTMPC_COST_TRACK (either may be NULL). */
+int dtmpc_ift_gradient(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
+                       const double* theta_raw, int64_t B, const void* X, const void* U,
+                       const void* dX, const void* dU, const void* dlam, const void* Xref,
+                       const void* Uref, void* g_theta, void* g_xref, void* g_uref, void* stream);
+
+/* Closed-loop configuration of the general path (core/tube_mpc.py:48-188). */
+typedef struct dtmpc_general_cfg {
+  double target[3];          /* DubinsConfig.x_target of the nominal cost */
+  dtmpc_ilqr_cfg nom_ilqr;   /* ILQRConfig(max_iter=nominal_max_iter, reg=ilqr_reg) (:161) */
+  dtmpc_ilqr_cfg aux_ilqr;   /* ILQRConfig(max_iter=aux_max_iter, reg=ilqr_reg) (:162) */
+  int32_t adapt_nominal;     /* (:108) */
+  int32_t adapt_ancillary;   /* (:109) */
+  int32_t project_params;    /* _project (:192-237) */
+  int32_t disturbance;       /* 0: injected w, 1: device Philox (as dtmpc_tube_cfg) */
+  int32_t write_log;
+  int32_t pad_;
+  uint64_t seed;
+  double w_low[3];
+  double w_high[3];
+  double lr_eta;             /* (:178) */
+  double momentum;           /* (:181) */
+  double clip_norm;          /* grad_clip_norm, per parameter tensor; <= 0 disables (:180) */
+} dtmpc_general_cfg;
+
+/* Device-resident state of the general closed loop; SoA [fields][B] unless stated. */
+typedef struct dtmpc_general_state {
+  void* x;          /* [3][B] */
+  void* b;          /* [B] */
+  void* xbar;       /* [3][B] */
+  void* bbar;       /* [B] */
+  void* Xnom;       /* [N+1][4][B] */
+  void* Unom;       /* [N][2][B] warm start in / optimum out (shifted by dtmpc_general_plant) */
+  void* Xaux;       /* [N+1][4][B] */
+  void* Uaux;       /* [N][2][B] */
+  void* work;       /* dtmpc_general_workspace_bytes() scratch */
+  void* theta;      /* [2][12] raw parameters, row 0 ancillary theta, row 1 nominal theta-bar
+                       (shared by the batch; updated in place by dtmpc_general_update) */
+  void* velocity;   /* [2][12] momentum buffers */
+  void* partials;   /* [nblocks][24] per-workgroup sums */
+  void* sums;       /* [24] batch sums (after the cross-rank all-reduce) */
+  void* gout;       /* [24][B] or NULL: each trajectory's own L and raw gradients */
+  void* log;        /* [12][B] or NULL: x(3) u(2) xbar(3) ubar(2) b L of step t */
+  int32_t* status;  /* [B] */
+  int32_t* iters;   /* [2][B] or NULL */
+} dtmpc_general_state;
+
+size_t dtmpc_general_workspace_bytes(int dtype, int32_t horizon, int64_t B);
+
+/* Solves + sensitivities + IFT gradients for every trajectory (core/tube_mpc.py:217-584):
+ * nominal iLQR with theta-bar -> ancillary iLQR tracking it with theta -> upper loss ->
+ * ancillary sensitivity -> ancillary IFT (theta, X_ref, U_ref) -> [adapt_nominal] nominal
+ * sensitivity driven by the reference gradients -> nominal IFT (theta-bar); per-workgroup sums of
+ * [L, g_theta(11), g_theta_bar(12)] into state->partials.  theta is read only. */
+int dtmpc_general_step(int dtype, const dtmpc_spec* spec, const dtmpc_general_cfg* cfg, int64_t B,
+                       const dtmpc_general_state* state, void* stream);
+
+/* Fixed-order sum of n_partials records of `width` values each into sums[width]. */
+int dtmpc_partials_reduce_n(int dtype, int64_t n_partials, int32_t width, const void* partials,
+                            void* sums, void* stream);
+
+/* Momentum / clipped / projected update of theta and theta-bar with the batch-mean gradient
+ * g = state->sums * inv_batch (core/tube_mpc.py:239-255, 507-508, 584). */
+int dtmpc_general_update(int dtype, const dtmpc_spec* spec, const dtmpc_general_cfg* cfg,
+                         double inv_batch, const dtmpc_general_state* state, void* stream);
+
+/* Plant step with the UPDATED parameters, nominal propagation, log, warm-start shift
+ * (core/tube_mpc.py:589-624).  w: [3][B] injected (cfg->disturbance == 0) or NULL. */
+int dtmpc_general_plant(int dtype, const dtmpc_spec* spec, const dtmpc_general_cfg* cfg, int64_t B,
+                        int64_t global_offset, int64_t step, const dtmpc_general_state* state,
+                        const void* w, void* stream);
 
 #ifdef __cplusplus
 }

@@ -71,22 +71,30 @@ static float ulpn_f(float v, float x) {
 #define D_SIN(x) ulpn_d(sin(x), (x))
 #define D_COS(x) ulpn_d(cos(x), (x) + 1.0)
 #define D_ATAN2(y, x) ulpn_d(atan2((y), (x)), (y))
+#define D_LOG1P(x) ulpn_d(log1p(x), (x))
+#define D_TANH(x) ulpn_d(tanh(x), (x))
 #define F_EXP(x) ulpn_f(expf(x), (x))
 #define F_LOG(x) ulpn_f(logf(x), (x))
 #define F_SIN(x) ulpn_f(sinf(x), (x))
 #define F_COS(x) ulpn_f(cosf(x), (x) + 1.0f)
 #define F_ATAN2(y, x) ulpn_f(atan2f((y), (x)), (y))
+#define F_LOG1P(x) ulpn_f(log1pf(x), (x))
+#define F_TANH(x) ulpn_f(tanhf(x), (x))
 #else
 #define D_EXP exp
 #define D_LOG log
 #define D_SIN sin
 #define D_COS cos
 #define D_ATAN2 atan2
+#define D_LOG1P log1p
+#define D_TANH tanh
 #define F_EXP expf
 #define F_LOG logf
 #define F_SIN sinf
 #define F_COS cosf
 #define F_ATAN2 atan2f
+#define F_LOG1P log1pf
+#define F_TANH tanhf
 #endif
 
 #define REAL double
@@ -96,6 +104,8 @@ static float ulpn_f(float v, float x) {
 #define M_SIN D_SIN
 #define M_COS D_COS
 #define M_ATAN2 D_ATAN2
+#define M_LOG1P D_LOG1P
+#define M_TANH D_TANH
 #define M_FABS fabs
 #include "oracle_impl.h"
 #undef REAL
@@ -105,6 +115,8 @@ static float ulpn_f(float v, float x) {
 #undef M_SIN
 #undef M_COS
 #undef M_ATAN2
+#undef M_LOG1P
+#undef M_TANH
 #undef M_FABS
 
 #define REAL float
@@ -114,5 +126,7 @@ static float ulpn_f(float v, float x) {
 #define M_SIN F_SIN
 #define M_COS F_COS
 #define M_ATAN2 F_ATAN2
+#define M_LOG1P F_LOG1P
+#define M_TANH F_TANH
 #define M_FABS fabsf
 #include "oracle_impl.h"

@@ -31,7 +31,7 @@ _libs: dict = {}
 
 
 def build(force: bool = False) -> str:
-    srcs = [os.path.join(HERE, f) for f in ("dtmpc_oracle.c", "oracle_impl.h", "Makefile")]
+    srcs = [os.path.join(HERE, f) for f in ("dtmpc_oracle.c", "oracle_impl.h", "oracle_general.h", "Makefile")]
     srcs.append(os.path.join(_REPO, "include", "dtmpc.h"))
     stale = force or any(
         not os.path.exists(p) or any(os.path.getmtime(s) > os.path.getmtime(p) for s in srcs) for p in LIB_PATHS.values())
@@ -190,6 +190,76 @@ class Oracle:
         sums, theta, vel = self._a(sums), self._a(theta).copy(), self._a(vel).copy()
         self._f("oracle_theta_update")(C.byref(adapt), C.c_double(inv_batch), _p(sums), _p(theta), _p(vel))
         return theta, vel
+
+
+    # ---- general (softplus / tanh parameterised) IFT path
+    def ddp_sensitivity_upper(self, spec, cost, X, V, gX, gU, want_lambda=True):
+        X = self._a(X)
+        B, N = X.shape[0], spec.horizon
+        Xs, Us, gx, gu = soa(X), soa(self._a(V)), soa(self._a(gX)), soa(self._a(gU))
+        dX = np.empty((N + 1, 4, B), self.dt)
+        dU = np.empty((N, 2, B), self.dt)
+        dL = np.empty((N + 1, 4, B), self.dt) if want_lambda else None
+        status = np.zeros(B, np.int32)
+        self._f("oracle_ddp_sensitivity_upper")(C.byref(spec), C.byref(cost), C.c_longlong(B), _p(Xs), _p(Us),
+                                                _p(gx), _p(gu), _p(dX), _p(dU), _p(dL), _p(status))
+        return aos(dX), aos(dU), (aos(dL) if dL is not None else None), status
+
+    def ift_gradient(self, spec, cost, theta_raw, X, V, dX, dV, dlam, Xref=None, Uref=None):
+        """-> g_theta [B, 12], g_xref [B, N+1, 3], g_uref [B, N, 2] (refs only for a tracking cost)"""
+        X = self._a(X)
+        B, N = X.shape[0], spec.horizon
+        th = (C.c_double * 12)(*[float(v) for v in np.asarray(theta_raw, np.float64).reshape(12)])
+        args = [soa(self._a(t)) for t in (X, V, dX, dV, dlam)]
+        Xr = soa(self._a(Xref)[..., :3]) if Xref is not None else None
+        Ur = soa(self._a(Uref)) if Uref is not None else None
+        g = np.zeros((12, B), self.dt)
+        gxr = np.zeros((N + 1, 3, B), self.dt)
+        gur = np.zeros((N, 2, B), self.dt)
+        self._f("oracle_ift_gradient")(C.byref(spec), C.byref(cost), th, C.c_longlong(B), *[_p(a) for a in args],
+                                       _p(Xr), _p(Ur), _p(g), _p(gxr), _p(gur))
+        return np.ascontiguousarray(g.T), aos(gxr), aos(gur)
+
+    def softplus(self, x):
+        x = self._a(x)
+        y = np.empty_like(x)
+        self._f("oracle_softplus")(C.c_longlong(x.size), _p(x), _p(y))
+        return y
+
+    def general_step(self, spec, gcfg, st: dict, theta):
+        """Solves + sensitivities + IFT for every trajectory; `st` SoA numpy arrays as tube_step.
+        theta [2, 12] raw.  Returns gout [24, B], status [B], iters [2, B]."""
+        B = st["b"].shape[0]
+        theta = np.ascontiguousarray(self._a(theta).reshape(2, 12))
+        gout = np.zeros((24, B), self.dt)
+        status = np.zeros(B, np.int32)
+        iters = np.zeros((2, B), np.int32)
+        for k in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux"):
+            assert st[k].dtype == self.dt and st[k].flags.c_contiguous, k
+        self._f("oracle_general_step")(C.byref(spec), C.byref(gcfg), C.c_longlong(B), _p(st["x"]), _p(st["b"]),
+                                       _p(st["xbar"]), _p(st["bbar"]), _p(st["Xnom"]), _p(st["Unom"]), _p(st["Xaux"]),
+                                       _p(st["Uaux"]), _p(theta), _p(gout), _p(status), _p(iters),
+                                       C.c_int(self.nthreads))
+        return gout, status, iters
+
+    def general_update(self, spec, gcfg, inv_batch, sums, theta, vel):
+        sums = self._a(sums)
+        theta = np.ascontiguousarray(self._a(theta).reshape(2, 12)).copy()
+        vel = np.ascontiguousarray(self._a(vel).reshape(2, 12)).copy()
+        self._f("oracle_general_update")(C.byref(spec), C.byref(gcfg), C.c_double(inv_batch), _p(sums), _p(theta),
+                                         _p(vel))
+        return theta, vel
+
+    def general_plant(self, spec, gcfg, st: dict, theta, L, w=None, goff: int = 0, step: int = 0, want_log=True):
+        B = st["b"].shape[0]
+        theta = np.ascontiguousarray(self._a(theta).reshape(2, 12))
+        ws = None if w is None else np.ascontiguousarray(self._a(w).T)
+        log = np.zeros((12, B), self.dt) if want_log else None
+        Ls = np.ascontiguousarray(self._a(L).reshape(B))
+        self._f("oracle_general_plant")(C.byref(spec), C.byref(gcfg), C.c_longlong(B), C.c_longlong(goff),
+                                        C.c_longlong(step), _p(st["x"]), _p(st["b"]), _p(st["xbar"]), _p(st["bbar"]),
+                                        _p(st["Unom"]), _p(st["Uaux"]), _p(theta), _p(Ls), _p(ws), _p(log))
+        return log
 
 
 def philox_bits(seed: int, gidx: int, step: int) -> np.ndarray:

@@ -27,6 +27,7 @@ typedef struct {
   REAL neg_beta, neg_inv_beta;
   REAL cx[DTMPC_MAX_OBS], cy[DTMPC_MAX_OBS], r2[DTMPC_MAX_OBS];
   REAL alpha, gamma, eps;
+  REAL tight; /* h offset of the DBaS dynamics (nominal tightening, core/tube_mpc.py:151-153) */
 } SPEC_T;
 
 typedef struct {
@@ -55,6 +56,7 @@ static void FN(spec_from)(const dtmpc_spec* s, SPEC_T* o) {
   o->alpha = (REAL)s->dbas_alpha;
   o->gamma = (REAL)s->dbas_gamma;
   o->eps = (REAL)s->dbas_eps;
+  o->tight = (REAL)s->h_offset;
 }
 
 static void FN(cost_from)(const dtmpc_cost* c, COST_T* o) {
@@ -189,8 +191,9 @@ static void FN(dubins)(const SPEC_T* s, const REAL* x, const REAL* u, REAL* xn) 
 static void FN(fhat)(const SPEC_T* s, const REAL* xh, const REAL* u, REAL* xhn) {
   REAL gx, gy;
   FN(dubins)(s, xh, u, xhn);
-  REAL hn = FN(h_eval)(s, xhn[0], xhn[1], &gx, &gy);
-  REAL hc = FN(h_eval)(s, xh[0], xh[1], &gx, &gy);
+  /* h_nom(x) = h(x) - s for the tightened nominal (core/tube_mpc.py:235-238); s = 0 otherwise */
+  REAL hn = FN(h_eval)(s, xhn[0], xhn[1], &gx, &gy) - s->tight;
+  REAL hc = FN(h_eval)(s, xh[0], xh[1], &gx, &gy) - s->tight;
   REAL Bn = FN(barrier_dyn)(s, hn);
   REAL Bc = FN(barrier_dyn)(s, hc);
   xhn[3] = Bn - s->gamma * (Bc - xh[3]);
@@ -558,9 +561,11 @@ static int FN(ilqr1)(const SPEC_T* s, const COST_T* c, const dtmpc_ilqr_cfg* cfg
 
 /* ---- DDP sensitivity (core/ddp.py:317-427) with the paper upper loss (core/tube_mpc.py:932-944) */
 
+/* Upper gradients: gX [N+1][4] / gU [N][2] when given (core/ddp.py:322-324 closures as arrays),
+ * else the paper upper loss g_x = [2(x - xbar_k), 2 b], g_u = 0. */
 static int FN(sens1)(const SPEC_T* s, const COST_T* c, const REAL* X, const REAL* V,
-                     const REAL* Xr, const REAL* Ur, const REAL* Xbar, REAL* dX, REAL* dV,
-                     REAL* dlam, REAL* work) {
+                     const REAL* Xr, const REAL* Ur, const REAL* Xbar, const REAL* gX,
+                     const REAL* gU, REAL* dX, REAL* dV, REAL* dlam, REAL* work) {
   (void)Ur;
   int N = s->N;
   REAL* Aseq = work;               /* N*16 */
@@ -583,8 +588,12 @@ static int FN(sens1)(const SPEC_T* s, const COST_T* c, const REAL* X, const REAL
   REAL Vxx[16], tVx[4];
   memset(Vxx, 0, sizeof(Vxx));
   for (int i = 0; i < 4; ++i) Vxx[5 * i] = pxx_d[i];
-  for (int i = 0; i < 3; ++i) tVx[i] = (REAL)2 * (X[4 * N + i] - Xbar[3 * N + i]);
-  tVx[3] = (REAL)2 * X[4 * N + 3];
+  if (gX) {
+    for (int i = 0; i < 4; ++i) tVx[i] = gX[4 * N + i];
+  } else {
+    for (int i = 0; i < 3; ++i) tVx[i] = (REAL)2 * (X[4 * N + i] - Xbar[3 * N + i]);
+    tVx[3] = (REAL)2 * X[4 * N + 3];
+  }
   memcpy(Vxxs + 16 * N, Vxx, sizeof(Vxx));
   memcpy(tVxs + 4 * N, tVx, sizeof(tVx));
   REAL reg = (REAL)1e-9;
@@ -630,13 +639,19 @@ static int FN(sens1)(const SPEC_T* s, const COST_T* c, const REAL* X, const REAL
         Quu[a * 2 + b] = (a == b ? luu_d[a] : (REAL)0) + acc;
       }
     /* g_u = 0, g_x = [2(x - xbar_k), 2 b] */
-    REAL gx[4];
-    for (int i = 0; i < 3; ++i) gx[i] = (REAL)2 * (X[4 * k + i] - Xbar[3 * k + i]);
-    gx[3] = (REAL)2 * X[4 * k + 3];
+    REAL gx[4], gu[2] = {0, 0};
+    if (gX) {
+      for (int i = 0; i < 4; ++i) gx[i] = gX[4 * k + i];
+      gu[0] = gU[2 * k];
+      gu[1] = gU[2 * k + 1];
+    } else {
+      for (int i = 0; i < 3; ++i) gx[i] = (REAL)2 * (X[4 * k + i] - Xbar[3 * k + i]);
+      gx[3] = (REAL)2 * X[4 * k + 3];
+    }
     for (int a = 0; a < 2; ++a) {
       REAL acc = 0;
       for (int m = 0; m < 4; ++m) acc += Bm[m * 2 + a] * tVx[m];
-      tQu[a] = (REAL)0 + acc;
+      tQu[a] = gu[a] + acc;
     }
     for (int i = 0; i < 4; ++i) {
       REAL acc = 0;
@@ -930,7 +945,7 @@ void FN(oracle_ddp_sensitivity)(const dtmpc_spec* sp, const dtmpc_cost* cp, long
       FN(gather)(X, N + 1, 4, B, i, Xa);
       FN(gather)(U, N, 2, B, i, Va);
       FN(gather)(Xbar, N + 1, 3, B, i, Xb);
-      int st = FN(sens1)(&s, &c, Xa, Va, NULL, NULL, Xb, dXa, dVa, dlam ? dla : NULL, wk);
+      int st = FN(sens1)(&s, &c, Xa, Va, NULL, NULL, Xb, NULL, NULL, dXa, dVa, dlam ? dla : NULL, wk);
       FN(scatter)(dXa, N + 1, 4, B, i, dX);
       FN(scatter)(dVa, N, 2, B, i, dU);
       if (dlam) FN(scatter)(dla, N + 1, 4, B, i, dlam);
@@ -1023,7 +1038,7 @@ void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long 
       FN(gather)(Uaux, N, 2, B, i, Va);
       st |= FN(ilqr1)(&s, &ca, &cfg->aux_ilqr, x0, Xr, Vn, Xa, Va, Ka, ka, &ita, wk);
       /* sensitivity + DOC gradient :915-976 */
-      st |= FN(sens1)(&s, &ca, Xa, Va, Xr, Vn, Xr, dXa, dVa, NULL, wk2);
+      st |= FN(sens1)(&s, &ca, Xa, Va, Xr, Vn, Xr, NULL, NULL, dXa, dVa, NULL, wk2);
       REAL o[7];
       FN(docgrad1)(N, Xa, Va, Xn, Vn, dXa, dVa, o);
       /* a flagged (non-finite) trajectory contributes nothing to the shared gradient */
@@ -1094,6 +1109,8 @@ void FN(oracle_theta_update)(const dtmpc_adapt_cfg* cfg, double inv_batch, const
     }
   }
 }
+
+#include "oracle_general.h"
 
 #undef SPEC_T
 #undef COST_T
