@@ -9,7 +9,8 @@ Reference mapping:
   rollout           core/ddp.py:89-99        -> dtmpc_dbas_rollout
   linearize         core/systems/dubins_aug_jac.py:61-139 + core/cost_derivs.py -> dtmpc_linearize
   ilqr_solve        core/ddp.py:102-307      -> dtmpc_ilqr_solve
-  ddp_sensitivity   core/ddp.py:317-427      -> dtmpc_ddp_sensitivity
+  ddp_sensitivity   core/ddp.py:317-427      -> dtmpc_ddp_sensitivity (paper upper loss) or
+                                                dtmpc_ddp_sensitivity_upper (upper gradients as arrays)
   doc_gradient      core/tube_mpc.py:915-976 -> dtmpc_doc_grad
 
 Errors follow the reference: FloatingPointError for non-finite values (core/ddp.py:138-159),
@@ -199,10 +200,19 @@ def ilqr_solve(*, problem: DubinsDBaSProblem, cost: QuadraticCost, cfg: ILQRConf
 
 
 def ddp_sensitivity(*, problem: DubinsDBaSProblem, cost: QuadraticCost, X: Tensor, V: Tensor,
-                    X_ref: Optional[Tensor], U_ref: Optional[Tensor], X_bar: Tensor,
+                    X_ref: Optional[Tensor] = None, U_ref: Optional[Tensor] = None, X_bar: Optional[Tensor] = None,
+                    upper_grad_x: Optional[Tensor] = None, upper_grad_u: Optional[Tensor] = None,
                     want_lambda: bool = True, check: bool = True) -> SensitivityResult:
-    """DDP-structured KKT sensitivity with active set (core/ddp.py:317-427) for the paper upper loss
-    L = sum ||x_k - xbar_k||^2 + b_k^2 (core/tube_mpc.py:915-957): g_x = [2(x - xbar), 2 b], g_u = 0."""
+    """DDP-structured KKT sensitivity with active set (core/ddp.py:317-427).
+
+    Upper-level gradients either as arrays -- upper_grad_x [B, N+1, 4] (row N = upper_grad_xN) and
+    upper_grad_u [B, N, 2], the reference's closures evaluated along the tape -- or, with X_bar, the
+    paper upper loss L = sum ||x_k - xbar_k||^2 + b_k^2 (core/tube_mpc.py:915-957):
+    g_x = [2(x - xbar), 2 b], g_u = 0."""
+    if upper_grad_x is not None or upper_grad_u is not None:
+        return _ddp_sensitivity_upper(problem, cost, X, V, upper_grad_x, upper_grad_u, want_lambda, check)
+    if X_bar is None:
+        raise ValueError("pass X_bar (paper upper loss) or upper_grad_x / upper_grad_u")
     _require_device(X, V, X_ref, U_ref, X_bar)
     B, N = X.shape[0], problem.horizon
     lib = _lib.load()
@@ -223,6 +233,34 @@ def ddp_sensitivity(*, problem: DubinsDBaSProblem, cost: QuadraticCost, X: Tenso
                                          _ptr(Xr), _ptr(Ur), Xb.data_ptr(), dX.data_ptr(), dU.data_ptr(), _ptr(dL),
                                          work.data_ptr(), status.data_ptr(), _lib.stream_of(X)),
                "dtmpc_ddp_sensitivity")
+    if check:
+        raise_for_status(status, "ddp_sensitivity")
+    return SensitivityResult(delta_X=from_soa(dX), delta_V=from_soa(dU),
+                             delta_lambda=from_soa(dL) if dL is not None else None)
+
+
+def _ddp_sensitivity_upper(problem, cost, X, V, gX, gU, want_lambda, check) -> SensitivityResult:
+    if gX is None or gU is None:
+        raise ValueError("upper_grad_x and upper_grad_u go together")
+    _require_device(X, V, gX, gU)
+    B, N = X.shape[0], problem.horizon
+    if gX.shape != (B, N + 1, 4) or gU.shape != (B, N, 2):
+        raise ValueError(f"upper_grad_x must be [{B}, {N + 1}, 4] and upper_grad_u [{B}, {N}, 2]")
+    lib = _lib.load()
+    spec, cc = problem.to_c(), cost.to_c()
+    dt = X.dtype
+    Xs, Us, gx, gu = to_soa(X), to_soa(V.to(dt)), to_soa(gX.to(dt)), to_soa(gU.to(dt))
+    kw = dict(dtype=dt, device=X.device)
+    dX = torch.empty(N + 1, 4, B, **kw)
+    dU = torch.empty(N, 2, B, **kw)
+    dL = torch.empty(N + 1, 4, B, **kw) if want_lambda else None
+    work = torch.empty(lib.dtmpc_sensitivity_upper_workspace_bytes(_dtype_code(X), N, B), dtype=torch.uint8,
+                       device=X.device)
+    status = torch.zeros(B, dtype=torch.int32, device=X.device)
+    _lib.check(lib.dtmpc_ddp_sensitivity_upper(_dtype_code(X), C.byref(spec), C.byref(cc), B, Xs.data_ptr(),
+                                               Us.data_ptr(), gx.data_ptr(), gu.data_ptr(), dX.data_ptr(),
+                                               dU.data_ptr(), _ptr(dL), work.data_ptr(), status.data_ptr(),
+                                               _lib.stream_of(X)), "dtmpc_ddp_sensitivity_upper")
     if check:
         raise_for_status(status, "ddp_sensitivity")
     return SensitivityResult(delta_X=from_soa(dX), delta_V=from_soa(dU),

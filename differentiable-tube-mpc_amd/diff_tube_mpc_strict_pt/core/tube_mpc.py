@@ -8,8 +8,13 @@
   per-workgroup gradient sums, a cross-rank all-reduce (RCCL) when the batch is sharded, and the
   momentum/projection update of theta (core/tube_mpc.py:978-984) with the batch-mean gradient.
   With B = 1 this is exactly the reference's loop body.
+* :class:`GeneralTubeMPC` — the same batched loop for the GENERAL path (core/tube_mpc.py:40-663):
+  softplus / tanh parameterised weights and DBaS parameters, both MPCs adapting by the IFT gradient
+  (the nominal one through the ancillary's reference-trajectory gradient).  One fused kernel for the
+  solves + sensitivities + IFT, a 24-float reduction / all-reduce, the clipped / momentum / projected
+  update, then the plant step with the updated parameters.
 * :func:`run_closed_loop_experiment` — signature- and output-compatible with the reference
-  (core/tube_mpc.py:40), for the configured paper mode (core/tube_mpc.py:666-1048).
+  (core/tube_mpc.py:40): the paper mode (core/tube_mpc.py:666-1048) or the general path.
 """
 from __future__ import annotations
 
@@ -25,9 +30,10 @@ from torch import Tensor
 
 from .. import _abi, _lib
 from .ddp import _dtype_code, raise_for_status
-from .problem import PaperSetup, paper_setup_from_config
+from .problem import GeneralSetup, PaperSetup, general_setup_from_config, paper_setup_from_config, softplus
 
-__all__ = ["ExperimentTrajectories", "TubeMPC", "run_closed_loop_experiment", "shard_range", "allreduce_sums"]
+__all__ = ["ExperimentTrajectories", "TubeMPC", "GeneralTubeMPC", "run_closed_loop_experiment", "shard_range",
+           "allreduce_sums"]
 
 
 @dataclass
@@ -210,6 +216,201 @@ class TubeMPC:
 
 
 # ---------------------------------------------------------------------------------------------
+class GeneralTubeMPC:
+    """Device-resident batched closed loop of the general path (core/tube_mpc.py:40-663).
+
+    theta [2, 12] (raw, DTMPC_P_* layout; row 0 ancillary, row 1 nominal) is shared by the batch
+    and updated with the batch-mean IFT gradient; at B = 1 every step is the reference's loop body.
+    Arguments as :class:`TubeMPC`."""
+
+    def __init__(self, setup, *, batch: int, device="cuda", dtype=torch.float32, disturbance: str = "philox",
+                 seed: int = 0, global_offset: int = 0, global_batch: Optional[int] = None, process_group=None,
+                 write_log: bool = False):
+        if isinstance(setup, dict):
+            setup = general_setup_from_config(setup)
+        self.setup: GeneralSetup = setup
+        if setup.adapt_steps != 1:
+            raise NotImplementedError("adaptation.steps != 1 is not supported (core/tube_mpc.py:401)")
+        self.B = int(batch)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("GeneralTubeMPC runs on a HIP device; there is no CPU fallback")
+        self.dtype = dtype
+        self.global_offset = int(global_offset)
+        self.global_batch = int(global_batch) if global_batch is not None else self.B
+        self.group = process_group
+        self.lib = _lib.load()
+        self.N = N = setup.problem.horizon
+        if disturbance not in ("philox", "injected"):
+            raise ValueError("disturbance must be 'philox' or 'injected'")
+        self._dt = _dtype_code(torch.empty(0, dtype=dtype))
+        self.spec = setup.problem.to_c()
+        self.cfg = setup.to_c(disturbance=1 if disturbance == "philox" else 0, seed=seed, write_log=write_log)
+        kw = dict(dtype=dtype, device=self.device)
+        B = self.B
+        self.x = torch.zeros(3, B, **kw)
+        self.b = torch.zeros(B, **kw)
+        self.xbar = torch.zeros(3, B, **kw)
+        self.bbar = torch.zeros(B, **kw)
+        self.Xnom = torch.zeros(N + 1, 4, B, **kw)
+        self.Unom = torch.zeros(N, 2, B, **kw)
+        self.Xaux = torch.zeros(N + 1, 4, B, **kw)
+        self.Uaux = torch.zeros(N, 2, B, **kw)
+        self.work = torch.empty(self.lib.dtmpc_general_workspace_bytes(self._dt, N, B), dtype=torch.uint8,
+                                device=self.device)
+        self.n_partials = int(self.lib.dtmpc_tube_partials_count(B))
+        self.partials = torch.zeros(self.n_partials, _abi.GEN_SUMS, **kw)
+        self.sums = torch.zeros(_abi.GEN_SUMS, **kw)
+        self._theta0 = torch.tensor(setup.theta0, **kw)
+        self.theta = self._theta0.clone()
+        self.vel = torch.zeros(2, _abi.P_COUNT, **kw)
+        self.gout = torch.zeros(_abi.GEN_SUMS, B, **kw)
+        self.status = torch.zeros(B, dtype=torch.int32, device=self.device)
+        self.iters = torch.zeros(2, B, dtype=torch.int32, device=self.device)
+        self.log = torch.zeros(_abi.GEN_LOG_FIELDS, B, **kw) if write_log else None
+        self.t = 0
+        st = _abi.DtmpcGeneralState()
+        st.x, st.b, st.xbar, st.bbar = (t.data_ptr() for t in (self.x, self.b, self.xbar, self.bbar))
+        st.Xnom, st.Unom, st.Xaux, st.Uaux = (t.data_ptr() for t in (self.Xnom, self.Unom, self.Xaux, self.Uaux))
+        st.work = self.work.data_ptr()
+        st.theta = self.theta.data_ptr()
+        st.velocity = self.vel.data_ptr()
+        st.partials = self.partials.data_ptr()
+        st.sums = self.sums.data_ptr()
+        st.gout = self.gout.data_ptr()
+        st.log = self.log.data_ptr() if self.log is not None else None
+        st.status = self.status.data_ptr()
+        st.iters = self.iters.data_ptr()
+        self.state = st
+
+    def _stream(self) -> int:
+        return int(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _spec_for(self, row, nominal: bool):
+        """spec with the DBaS parameters of a raw row (core/tube_mpc.py:134-153)"""
+        import dataclasses
+
+        p = dataclasses.replace(self.setup.problem, dbas_alpha=softplus(float(row[9])) + 1e-6,
+                                dbas_gamma=math.tanh(float(row[10])))
+        sp = p.to_c()
+        sp.h_offset = softplus(float(row[11])) if nominal else 0.0
+        return sp
+
+    def reset(self, x0: Tensor, U_nom0: Optional[Tensor] = None, U_aux0: Optional[Tensor] = None) -> None:
+        """x0 [B, 3]: plant and nominal start at x0; b0 = B_theta(h(x0)), bbar0 = B_theta_bar(h(x0) - s)
+        (core/tube_mpc.py:157-158); warm starts zero; theta / momentum restart from the setup."""
+        if x0.shape != (self.B, 3):
+            raise ValueError(f"x0 must be [{self.B}, 3]")
+        xs = x0.to(device=self.device, dtype=self.dtype).t().contiguous()
+        self.x.copy_(xs)
+        self.xbar.copy_(xs)
+        s = self._stream()
+        for row, nominal, out in ((self.setup.theta0[0], False, self.b), (self.setup.theta0[1], True, self.bbar)):
+            sp = self._spec_for(row, nominal)
+            _lib.check(self.lib.dtmpc_dbas_init(self._dt, C.byref(sp), self.B, self.x.data_ptr(), out.data_ptr(), s),
+                       "dtmpc_dbas_init")
+        self.Unom.zero_()
+        self.Uaux.zero_()
+        if U_nom0 is not None:
+            self.Unom.copy_(U_nom0.to(self.Unom).permute(1, 2, 0))
+        if U_aux0 is not None:
+            self.Uaux.copy_(U_aux0.to(self.Uaux).permute(1, 2, 0))
+        self.theta.copy_(self._theta0)
+        self.vel.zero_()
+        self.status.zero_()
+        self.t = 0
+
+    def step(self, w: Optional[Tensor] = None, kernel_events=None) -> None:
+        """One closed-loop step of the general path for the whole batch (asynchronous)."""
+        wp = None
+        if self.cfg.disturbance == 0:
+            if w is None or w.shape != (self.B, 3):
+                raise ValueError(f"injected disturbance w must be [{self.B}, 3]")
+            self._w = w.to(device=self.device, dtype=self.dtype).t().contiguous()
+            wp = self._w.data_ptr()
+        s = self._stream()
+        if kernel_events is not None:
+            kernel_events[0].record()
+        _lib.check(self.lib.dtmpc_general_step(self._dt, C.byref(self.spec), C.byref(self.cfg), self.B,
+                                               C.byref(self.state), s), "dtmpc_general_step")
+        if kernel_events is not None:
+            kernel_events[1].record()
+        _lib.check(self.lib.dtmpc_partials_reduce_n(self._dt, self.n_partials, _abi.GEN_SUMS,
+                                                    self.partials.data_ptr(), self.sums.data_ptr(), s),
+                   "dtmpc_partials_reduce_n")
+        allreduce_sums(self.sums, self.group)
+        _lib.check(self.lib.dtmpc_general_update(self._dt, C.byref(self.spec), C.byref(self.cfg),
+                                                 1.0 / self.global_batch, C.byref(self.state), s),
+                   "dtmpc_general_update")
+        _lib.check(self.lib.dtmpc_general_plant(self._dt, C.byref(self.spec), C.byref(self.cfg), self.B,
+                                                self.global_offset, self.t, C.byref(self.state), wp, s),
+                   "dtmpc_general_plant")
+        self.t += 1
+
+    def check(self) -> None:
+        raise_for_status(self.status, "general tube step")
+
+    @property
+    def loss_mean(self) -> float:
+        return float(self.sums[0]) / self.global_batch
+
+
+def _save_outputs(run_dir: str, traj: ExperimentTrajectories) -> None:
+    """core/tube_mpc.py:626-636"""
+    os.makedirs(run_dir, exist_ok=True)
+    np.save(os.path.join(run_dir, "x_real.npy"), np.stack(traj.x_real, axis=0))
+    np.save(os.path.join(run_dir, "u_real.npy"), np.stack(traj.u_real, axis=0))
+    np.save(os.path.join(run_dir, "x_bar.npy"), np.stack(traj.x_bar, axis=0))
+    np.save(os.path.join(run_dir, "u_bar.npy"), np.stack(traj.u_bar, axis=0))
+    np.save(os.path.join(run_dir, "b_real.npy"), np.stack(traj.b_real, axis=0))
+    np.save(os.path.join(run_dir, "loss.npy"), np.asarray(traj.loss, dtype=np.float64))
+    if len(traj.Qa_history) > 0:
+        np.save(os.path.join(run_dir, "Qa_history.npy"), np.stack(traj.Qa_history, axis=0))
+        np.save(os.path.join(run_dir, "Ra_history.npy"), np.stack(traj.Ra_history, axis=0))
+        np.save(os.path.join(run_dir, "qba_history.npy"), np.asarray(traj.qba_history, dtype=np.float64))
+
+
+def _run_general(cfg: Dict[str, Any], *, device, run_dir: str) -> Dict[str, Any]:
+    """General path of core/tube_mpc.py:40-663 for one trajectory on the HIP device."""
+    setup = general_setup_from_config(cfg)
+    dtype = torch.float64 if setup.use_float64 else torch.float32
+    H = setup.task_horizon
+    mpc = GeneralTubeMPC(setup, batch=1, device=device, dtype=dtype, disturbance="injected", write_log=True)
+    mpc.reset(torch.tensor([list(setup.x0)], dtype=dtype, device=device))
+    low = torch.tensor(setup.w_low, device=device, dtype=dtype)
+    high = torch.tensor(setup.w_high, device=device, dtype=dtype)
+    logs = torch.zeros(H, _abi.GEN_LOG_FIELDS, dtype=dtype, device=device)
+    thetas = torch.zeros(H, 2, _abi.P_COUNT, dtype=dtype, device=device)
+    probe = torch.empty(1, 3, device=device, dtype=dtype)
+    for t in range(H):
+        if (t % 25) == 0:
+            print(f"[step {t}/{H}] running...", flush=True)
+        w = low + (high - low) * torch.rand_like(probe)
+        mpc.step(w)
+        logs[t].copy_(mpc.log[:, 0])
+        thetas[t].copy_(mpc.theta)
+    mpc.check()
+    lg = logs.cpu().numpy()
+    th = torch.nn.functional.softplus(thetas[:, 0]).cpu().numpy()  # theta.Q() etc. (:611-614)
+    traj = ExperimentTrajectories(
+        x_real=list(lg[:, 0:3]), u_real=list(lg[:, 3:5]), x_bar=list(lg[:, 5:8]), u_bar=list(lg[:, 8:10]),
+        loss=[float(v) for v in lg[:, 11]], b_real=list(lg[:, 10]),
+        Qa_history=list(th[:, 0:3]) if setup.adapt_ancillary else [],
+        Ra_history=list(th[:, 3:5]) if setup.adapt_ancillary else [],
+        qba_history=[float(v) for v in th[:, 8]] if setup.adapt_ancillary else [])
+    _save_outputs(run_dir, traj)
+    summary = {
+        "system": "dubins",
+        "H": H,
+        "N": setup.problem.horizon,
+        "final_state": np.asarray(traj.x_real[-1]).tolist(),
+        "final_barrier_state": float(np.array(traj.b_real[-1]).reshape(-1)[0]),
+        "final_loss": float(traj.loss[-1]),
+    }
+    return {"summary": summary}
+
+
+# ---------------------------------------------------------------------------------------------
 def run_closed_loop_experiment(cfg: Dict[str, Any], *, device: torch.device, run_dir: str) -> Dict[str, Any]:
     """Drop-in for core/tube_mpc.py:40 in the configured paper mode (core/tube_mpc.py:666-1048).
 
@@ -220,12 +421,10 @@ def run_closed_loop_experiment(cfg: Dict[str, Any], *, device: torch.device, run
     if system_cfg["name"] != "dubins":
         raise NotImplementedError("Only dubins is wired in the skeleton; other systems are added next.")
     paper_mode = bool(cfg.get("paper_dubins_mode", True))
-    adapt_nominal = bool(cfg.get("adaptation", {}).get("adapt_nominal", False))
-    if not paper_mode or adapt_nominal:
-        raise NotImplementedError(
-            "the general (softplus-parameterised, adapt_nominal) IFT path of core/tube_mpc.py:40-663 is not "
-            "part of this build's hot path yet (SURVEY.md §8f-1); use the paper mode")
+    adapt_nominal = bool(cfg.get("adaptation", {}).get("adapt_nominal", True))
     device = torch.device(device)
+    if not (paper_mode and not adapt_nominal):  # core/tube_mpc.py:48-49
+        return _run_general(cfg, device=device, run_dir=run_dir)
     setup = paper_setup_from_config(cfg)
     dtype = torch.float64 if setup.use_float64 else torch.float32
     H = setup.task_horizon
@@ -251,16 +450,7 @@ def run_closed_loop_experiment(cfg: Dict[str, Any], *, device: torch.device, run
         x_real=list(lg[:, 0:3]), u_real=list(lg[:, 3:5]), x_bar=list(lg[:, 5:8]), u_bar=list(lg[:, 8:10]),
         loss=[float(v) for v in lg[:, 11]], b_real=list(lg[:, 10]), Qa_history=list(th[:, 0:3]),
         Ra_history=list(th[:, 3:5]), qba_history=[float(v) for v in th[:, 5]])
-    os.makedirs(run_dir, exist_ok=True)
-    np.save(os.path.join(run_dir, "x_real.npy"), np.stack(traj.x_real, axis=0))
-    np.save(os.path.join(run_dir, "u_real.npy"), np.stack(traj.u_real, axis=0))
-    np.save(os.path.join(run_dir, "x_bar.npy"), np.stack(traj.x_bar, axis=0))
-    np.save(os.path.join(run_dir, "u_bar.npy"), np.stack(traj.u_bar, axis=0))
-    np.save(os.path.join(run_dir, "b_real.npy"), np.stack(traj.b_real, axis=0))
-    np.save(os.path.join(run_dir, "loss.npy"), np.asarray(traj.loss, dtype=np.float64))
-    np.save(os.path.join(run_dir, "Qa_history.npy"), np.stack(traj.Qa_history, axis=0))
-    np.save(os.path.join(run_dir, "Ra_history.npy"), np.stack(traj.Ra_history, axis=0))
-    np.save(os.path.join(run_dir, "qba_history.npy"), np.asarray(traj.qba_history, dtype=np.float64))
+    _save_outputs(run_dir, traj)
     summary = {
         "system": "dubins",
         "H": H,
