@@ -151,6 +151,19 @@ __device__ __forceinline__ T h_circle(const DSpec<T>&, int i, T px, T py) {  // 
   return dx * dx + dy * dy - k.r2[i];
 }
 
+// h_i rounded as the reference rounds it (dx*dx, dy*dy, their sum, minus r^2: no fused multiply-add).
+// Used where h_i decides a discrete choice -- the exact-min argmin and the collision test: on a
+// symmetric obstacle field (e.g. x = y with obstacles mirrored about the diagonal) two h_i tie up to
+// an ulp and a contracted fma(dx, dx, dy*dy) picks the other obstacle than the reference does.
+template <typename T>
+__device__ __forceinline__ T h_circle_exact(const DSpec<T>&, int i, T px, T py) {
+#pragma clang fp contract(off)
+  const DSpec<T>& k = kspec<T>();
+  T dx = px - k.cx[i];
+  T dy = py - k.cy[i];
+  return dx * dx + dy * dy - k.r2[i];
+}
+
 // h for W points at once (obstacle loop outer, points inner => W-wide ILP).
 //   smoothmin: h_multi_circle_obstacles :41-69 (stable LSE, two passes)
 //   min:       h_min_circle_obstacles :95-106
@@ -211,17 +224,17 @@ __device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* p
     for (int w = 0; w < W; ++w) h[w] = s.neg_inv_beta * (zmax[w] + m_log(se[w]));
   } else if (s.agg == DTMPC_OBS_MIN && s.M > 0) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) h[w] = h_circle(s, 0, px[w], py[w]);
+    for (int w = 0; w < W; ++w) h[w] = h_circle_exact(s, 0, px[w], py[w]);
     for (int i = 1; i < s.M; ++i) {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        T hi = h_circle(s, i, px[w], py[w]);
+        T hi = h_circle_exact(s, i, px[w], py[w]);
         h[w] = hi < h[w] ? hi : h[w];
       }
     }
   } else if (s.agg == DTMPC_OBS_SINGLE && s.M > 0) {
 #pragma unroll
-    for (int w = 0; w < W; ++w) h[w] = h_circle(s, 0, px[w], py[w]);
+    for (int w = 0; w < W; ++w) h[w] = h_circle_exact(s, 0, px[w], py[w]);
   } else {
 #pragma unroll
     for (int w = 0; w < W; ++w) h[w] = T(1);
@@ -292,9 +305,9 @@ __device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy)
   }
   if (s.agg == DTMPC_OBS_MIN && s.M > 0) {
     int am = 0;
-    T hm = h_circle(s, 0, px, py);
+    T hm = h_circle_exact(s, 0, px, py);
     for (int i = 1; i < s.M; ++i) {
-      T hi = h_circle(s, i, px, py);
+      T hi = h_circle_exact(s, i, px, py);
       if (hi < hm) {
         hm = hi;
         am = i;
@@ -307,7 +320,7 @@ __device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy)
   if (s.agg == DTMPC_OBS_SINGLE && s.M > 0) {
     gx = T(2) * (px - kspec<T>().cx[0]);
     gy = T(2) * (py - kspec<T>().cy[0]);
-    return h_circle(s, 0, px, py);
+    return h_circle_exact(s, 0, px, py);
   }
   gx = T(0);
   gy = T(0);

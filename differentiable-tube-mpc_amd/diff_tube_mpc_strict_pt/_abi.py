@@ -206,6 +206,10 @@ PROTOTYPES = {
     "dtmpc_general_plant": (
         C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcGeneralCfg), I64, I64, I64,
                   C.POINTER(DtmpcGeneralState), P, P]),
+    "dtmpc_receding_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64]),
+    "dtmpc_nominal_receding": (
+        C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, I32, C.c_double,
+                  P, P, P, P, P, P, P, P, P]),
 }
 
 

@@ -60,13 +60,15 @@ def _require_device(*ts: Tensor) -> None:
 
 
 def to_soa(t: Tensor) -> Tensor:
-    """[B, rows, F] -> contiguous [rows, F, B]."""
-    return t.permute(1, 2, 0).contiguous()
+    """[B, rows, F] -> contiguous [rows, F, B], always a fresh buffer: at B = 1 the permuted view is
+    already "contiguous" and .contiguous() would hand the caller's own storage to kernels that write
+    their in/out arrays (V_init must never be mutated, core/ddp.py:127)."""
+    return t.permute(1, 2, 0).clone(memory_format=torch.contiguous_format)
 
 
 def from_soa(t: Tensor) -> Tensor:
     """[rows, F, B] -> [B, rows, F] (contiguous copy)."""
-    return t.permute(2, 0, 1).contiguous()
+    return t.permute(2, 0, 1).clone(memory_format=torch.contiguous_format)
 
 
 def _ptr(t: Optional[Tensor]) -> Optional[int]:

@@ -367,6 +367,23 @@ int dtmpc_general_plant(int dtype, const dtmpc_spec* spec, const dtmpc_general_c
                         int64_t global_offset, int64_t step, const dtmpc_general_state* state,
                         const void* w, void* stream);
 
+/* ---- receding-horizon nominal MPC (run_nominal.py:204-415) --------------------------------- */
+
+size_t dtmpc_receding_workspace_bytes(int dtype, int32_t horizon, int64_t B);
+
+/* B independent runs of run_nominal_receding, the whole task horizon H in one launch: per step
+ * iLQR (cost: nominal, usually wrap_angle = 1, run_nominal.py:297-324) from [x_t, b_t] with the
+ * shifted warm start -> u0 -> x_{t+1} = f_hat(x_t, u0) -> exits: collision when the true
+ * min_i h_i(x_t) <= 0 (:388-397), success when ||x_t[:2] - target[:2]|| <= success_radius
+ * (:399-403).  x0 [3][B] (b0 = B(h(x0)) is derived, :279); U [N][2][B] warm start in (the reference
+ * uses v = v_max, omega = 0, :368-369), last shifted plan out; log [H][6][B] out: x(3), u0(2), b of
+ * every recorded step (rows past h_ran untouched); h_ran / success_t (-1: none) / collided [B] out;
+ * status [B] OR-accumulated (a failed solve ends that trajectory's run, where the reference raises). */
+int dtmpc_nominal_receding(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
+                           const dtmpc_ilqr_cfg* cfg, int64_t B, int32_t H, double success_radius,
+                           const void* x0, void* U, void* log, int32_t* h_ran, int32_t* success_t,
+                           int32_t* collided, int32_t* status, void* work, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,13 +53,15 @@ def _p(a):
 
 
 def soa(a: np.ndarray) -> np.ndarray:
-    """[B, rows, F] -> contiguous [rows, F, B]"""
-    return np.ascontiguousarray(np.transpose(a, (1, 2, 0)))
+    """[B, rows, F] -> contiguous [rows, F, B], always a copy (at B = 1 the transpose is already
+    C-contiguous and ascontiguousarray would alias the caller's array, which the in/out buffers then
+    overwrite)"""
+    return np.array(np.transpose(a, (1, 2, 0)), order="C", copy=True)
 
 
 def aos(a: np.ndarray) -> np.ndarray:
-    """[rows, F, B] -> [B, rows, F]"""
-    return np.ascontiguousarray(np.transpose(a, (2, 0, 1)))
+    """[rows, F, B] -> [B, rows, F] (a copy)"""
+    return np.array(np.transpose(a, (2, 0, 1)), order="C", copy=True)
 
 
 class Oracle:
@@ -260,6 +262,21 @@ class Oracle:
                                         C.c_longlong(step), _p(st["x"]), _p(st["b"]), _p(st["xbar"]), _p(st["bbar"]),
                                         _p(st["Unom"]), _p(st["Uaux"]), _p(theta), _p(Ls), _p(ws), _p(log))
         return log
+
+
+    def nominal_receding(self, spec, cost, cfg, x0, H, success_r, U_ws):
+        """run_nominal.py:204-415 for B starts x0 [B, 3]; U_ws [B, N, 2] warm starts.
+        -> log [B, H, 6] (x, u0, b), h_ran, success_t, collided, status [B], last plans [B, N, 2]"""
+        x0 = self._a(x0)
+        B, N = x0.shape[0], spec.horizon
+        xs = np.ascontiguousarray(x0.T)
+        Us = soa(self._a(U_ws))
+        log = np.full((H, 6, B), np.nan, self.dt)
+        h_ran, st_t, coll, status = (np.zeros(B, np.int32) for _ in range(4))
+        self._f("oracle_nominal_receding")(C.byref(spec), C.byref(cost), C.byref(cfg), C.c_longlong(B), C.c_int(H),
+                                           C.c_double(success_r), _p(xs), _p(Us), _p(log), _p(h_ran), _p(st_t),
+                                           _p(coll), _p(status), C.c_int(self.nthreads))
+        return aos(log), h_ran, st_t, coll, status, aos(Us)
 
 
 def philox_bits(seed: int, gidx: int, step: int) -> np.ndarray:

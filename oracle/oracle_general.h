@@ -5,7 +5,8 @@
  * parameterised weights and DBaS parameters (core/params.py:9-59), the ancillary and nominal IFT
  * gradients of core/ift.py:35-92 in closed form, the reference-trajectory gradients that drive the
  * nominal sensitivity (core/tube_mpc.py:509-554), the clipped / momentum / projected update
- * (:239-255) and the plant step with the updated parameters (:589-600).
+ * (:239-255) and the plant step with the updated parameters (:589-600).  Also the receding-horizon
+ * nominal MPC driver of run_nominal.py:204-415 (oracle_nominal_receding, at the end).
  *
  * Closed forms of the autograd quantities (per step k < N, with x' = f(x_k, u_k)):
  *   cost:      d/dQ_i [l_x . dx_k] = 2 (x_k - r_k)_i dx_k,i,  d/dR_j [l_u . du_k] = 2 (u_k - q_k)_j du_k,j,
@@ -496,3 +497,84 @@ void FN(oracle_general_plant)(const dtmpc_spec* sp, const dtmpc_general_cfg* cfg
 }
 
 #undef GPAR_T
+
+/* ---- receding-horizon nominal MPC (run_nominal.py:204-415) ----------------------------------- */
+
+/* true min_i h_i(x) over the circles (run_nominal.py:390-396; h_circle_obstacle :16-30) */
+static REAL FN(h_true_min)(const SPEC_T* s, REAL px, REAL py) {
+  REAL m = FN(h_circle)(s, 0, px, py);
+  for (int i = 1; i < s->M; ++i) {
+    REAL hi = FN(h_circle)(s, i, px, py);
+    m = hi < m ? hi : m;
+  }
+  return m;
+}
+
+/* B independent receding-horizon runs from x0 [3][B] with warm starts Uws [N][2][B] (in: the
+ * v = v_max rows of run_nominal.py:368-369; out: the last shifted plan).  log [H][6][B]: x(3), u0(2), b
+ * per recorded step.  h_ran / success_t (-1 = none) / collided / status per trajectory. */
+void FN(oracle_nominal_receding)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cfg, long long B,
+                                 int H, double success_r, const REAL* x0, REAL* Uws, REAL* log, int* h_ran,
+                                 int* success_t, int* collided, int* status, int nthreads) {
+  SPEC_T s;
+  COST_T c;
+  FN(spec_from)(sp, &s);
+  FN(cost_from)(cp, &c);
+  int N = s.N;
+  int has_obs = s.agg != DTMPC_OBS_NONE && s.M > 0;
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+  {
+    size_t per = (size_t)(4 * (N + 1) + 2 * N + 8 * N + 2 * N + 2 * (4 * (N + 1) + 2 * N) + 16);
+    REAL* buf = (REAL*)malloc(sizeof(REAL) * per);
+    REAL* X = buf;
+    REAL* V = X + 4 * (N + 1);
+    REAL* K = V + 2 * N;
+    REAL* kf = K + 8 * N;
+    REAL* wk = kf + 2 * N;
+#pragma omp for schedule(dynamic, 1)
+    for (long long i = 0; i < B; ++i) {
+      REAL xh[4], gx, gy;
+      for (int f = 0; f < 3; ++f) xh[f] = x0[(long long)f * B + i];
+      /* b = dbas_init_b0(x, h, db_cfg) (:279) */
+      xh[3] = FN(barrier_dyn)(&s, FN(h_eval)(&s, xh[0], xh[1], &gx, &gy) - s.tight);
+      FN(gather)(Uws, N, 2, B, i, V);
+      int st = 0, ran = H, sidx = -1, coll = 0;
+      for (int t = 0; t < H; ++t) {
+        int it = 0;
+        REAL x0h[4] = {xh[0], xh[1], xh[2], xh[3]};
+        st |= FN(ilqr1)(&s, &c, cfg, x0h, NULL, NULL, X, V, K, kf, &it, wk);
+        REAL u0[2] = {V[0], V[1]}, xn[4];
+        FN(fhat)(&s, xh, u0, xn);
+        REAL rec[6] = {xh[0], xh[1], xh[2], u0[0], u0[1], xh[3]};
+        for (int f = 0; f < 6; ++f) log[((long long)t * 6 + f) * B + i] = rec[f];
+        if (st) {
+          ran = t + 1;
+          break;
+        }
+        if (has_obs && FN(h_true_min)(&s, xh[0], xh[1]) <= 0) { /* :388-397 */
+          coll = 1;
+          ran = t + 1;
+          break;
+        }
+        REAL ex = xh[0] - c.target[0], ey = xh[1] - c.target[1];
+        if (sqrt((double)(ex * ex + ey * ey)) <= success_r) { /* :399-403 */
+          sidx = t;
+          ran = t + 1;
+          break;
+        }
+        for (int k = 0; k + 1 < N; ++k) { /* :405-406 */
+          V[2 * k] = V[2 * (k + 1)];
+          V[2 * k + 1] = V[2 * (k + 1) + 1];
+        }
+        for (int f = 0; f < 4; ++f) xh[f] = xn[f];
+      }
+      FN(scatter)(V, N, 2, B, i, Uws);
+      h_ran[i] = ran;
+      success_t[i] = sidx;
+      collided[i] = coll;
+      if (status) status[i] |= st;
+    }
+    free(buf);
+  }
+}
