@@ -40,7 +40,8 @@ def build(force: bool = False, variant: str = "", defines=()) -> str:
     procs = []
     for src in SRCS:
         obj = out + "." + os.path.splitext(os.path.basename(src))[0] + ".o"
-        cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-c", "-o", obj, src]
+        extra = os.environ.get("DTMPC_EXTRA_FLAGS", "").split() if variant else []
+        cmd = [HIPCC, *FLAGS, *extra, *[f"-D{d}" for d in defines], "-c", "-o", obj, src]
         print("[build]", " ".join(cmd), flush=True)
         procs.append(subprocess.Popen(cmd))
         objs.append(obj)

@@ -126,6 +126,8 @@ struct Col {
   T* base;
   unsigned ld;    // B
   unsigned lane;  // trajectory index
+  // (A raw-buffer-resource form of this accessor -- SGPR plane base, no VALU address add per access --
+  // measured 10 % SLOWER on the tube step: the extra SGPRs per live descriptor deepen the SGPR spill.)
   __device__ __forceinline__ T& at(int k, int F, int f) const {
     return (base + (size_t)((unsigned)(k * F + f) * ld))[lane];
   }
@@ -168,9 +170,9 @@ __device__ __forceinline__ T h_circle_exact(const DSpec<T>&, int i, T px, T py) 
 //   smoothmin: h_multi_circle_obstacles :41-69 (stable LSE, two passes)
 //   min:       h_min_circle_obstacles :95-106
 //   single:    h_circle_obstacle :16-30;  none: 1 (run_nominal.py:256)
-// The value path keeps a runtime obstacle loop: specialising it on a compile-time count (tried in
-// round 1, both as register-held z_i and as recomputed passes) made the compiler copy the by-value
-// spec to scratch and tripled the line-search cost.  h_grad (W = 1) is specialised below.
+// Obstacle counts up to kFastObs are specialised at compile time (a wave-uniform switch; the table is
+// read in place from the kernarg segment, kspec(), so the by-value spec is never copied to scratch);
+// larger counts take the runtime obstacle loop.
 constexpr int kFastObs = 8;
 
 template <typename T, int MO>
@@ -185,8 +187,49 @@ __device__ __forceinline__ T h_smoothmin1(const DSpec<T>& s, T px, T py) {
   return s.neg_inv_beta * (zmax + m_log(se));
 }
 
+// W points, compile-time obstacle count: the h_i of the first (max) pass are kept in registers for
+// the exp pass instead of being recomputed (same values, same rounding).  Line search (W = NC):
+// tube step 8.14 -> 7.48 ms at B = 65,536 (round 1, v6).
+template <typename T, int W, int MO>
+__device__ __forceinline__ void h_smoothmin_w(const DSpec<T>& s, const T* px, const T* py, T* h) {
+  T hi[MO][W], hm[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) hm[w] = hi[0][w] = h_circle(s, 0, px[w], py[w]);
+#pragma unroll
+  for (int i = 1; i < MO; ++i)
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      hi[i][w] = h_circle(s, i, px[w], py[w]);
+      hm[w] = m_min(hm[w], hi[i][w]);
+    }
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const T zmax = s.neg_beta * hm[w];
+    T se = T(0);
+#pragma unroll
+    for (int i = 0; i < MO; ++i) se += m_exp(s.neg_beta * hi[i][w] - zmax);
+    h[w] = s.neg_inv_beta * (zmax + m_log(se));
+  }
+}
+
 template <typename T, int W>
 __device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* py, T* h) {
+#ifndef DTMPC_LS_RUNTIME_OBS
+  if constexpr (W > 1) {
+    if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0 && s.M <= kFastObs) {
+      switch (s.M) {  // wave-uniform
+        case 1: h_smoothmin_w<T, W, 1>(s, px, py, h); return;
+        case 2: h_smoothmin_w<T, W, 2>(s, px, py, h); return;
+        case 3: h_smoothmin_w<T, W, 3>(s, px, py, h); return;
+        case 4: h_smoothmin_w<T, W, 4>(s, px, py, h); return;
+        case 5: h_smoothmin_w<T, W, 5>(s, px, py, h); return;
+        case 6: h_smoothmin_w<T, W, 6>(s, px, py, h); return;
+        case 7: h_smoothmin_w<T, W, 7>(s, px, py, h); return;
+        default: h_smoothmin_w<T, W, 8>(s, px, py, h); return;
+      }
+    }
+  }
+#endif
   if constexpr (W == 1) {
     // single point (commit / rollout / plant): a dependent chain, so the compile-time count matters
     if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0 && s.M <= kFastObs) {

@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(kBlock) ift_kernel(DSpec<T> s, DCost<T> c, Raw
         Gu.at(k, 2, 1) = -(T(2) * p.R[1]) * duk[1];
       }
     }
-    ift_step(sp, xk, uk, dxk, duk, dL.at(k + 1, 4, 3), r, q, A);
+    ift_step(sp, xk, uk, dxk, duk, T(dL.at(k + 1, 4, 3)), r, q, A);
   }
   T xN[4] = {X.at(N, 4, 0), X.at(N, 4, 1), X.at(N, 4, 2), X.at(N, 4, 3)};
   T dxN[4] = {dX.at(N, 4, 0), dX.at(N, 4, 1), dX.at(N, 4, 2), dX.at(N, 4, 3)};
@@ -406,7 +406,7 @@ static int launch_general(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int
   case n:                                                                                                \
     hipLaunchKernelGGL((general_step_kernel<T, n>), grid_for(B), dim3(kBlock), 0, st, s, cfn, cfa, a); \
     break;
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+    DTMPC_NA_CASES(CASE)
 #undef CASE
     default: return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
   }

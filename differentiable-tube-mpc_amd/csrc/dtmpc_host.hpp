@@ -14,6 +14,15 @@ namespace dtmpc {
 
 constexpr int kBlock = 256;
 
+// Line-search candidate counts the kernels are instantiated for (1..8).  -DDTMPC_NA_ONLY=n builds
+// only n (experiment variants of the library: a quarter of the compile time; other counts then
+// return DTMPC_ERR_BAD_ARG).
+#ifdef DTMPC_NA_ONLY
+#define DTMPC_NA_CASES(C) C(DTMPC_NA_ONLY)
+#else
+#define DTMPC_NA_CASES(C) C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8)
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // host-side conversion of the C structs into the typed device descriptors
 template <typename T>

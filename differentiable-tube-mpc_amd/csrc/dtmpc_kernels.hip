@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(kBlock) linearize_kernel(DSpec<T> s, DCost<T> 
     }
   }
   load_ref(c, Xr, 3, N, r0, r1, r2);
-  deriv_dx(c, X.at(N, 4, 0), X.at(N, 4, 1), X.at(N, 4, 2), r0, r1, r2, d0, d1, d2);
+  deriv_dx(c, T(X.at(N, 4, 0)), T(X.at(N, 4, 1)), T(X.at(N, 4, 2)), r0, r1, r2, d0, d1, d2);
   LX.at(N, 4, 0) = pxx[0] * d0;
   LX.at(N, 4, 1) = pxx[1] * d1;
   LX.at(N, 4, 2) = pxx[2] * d2;
@@ -385,7 +385,7 @@ static int launch_ilqr(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_i
   switch (cfg.nc) {  // rolled-out candidates (alpha = 0 is taken from the previous iteration)
 #define CASE(n) \
   case n: launch_ilqr_na<T, n>(s, c, cfg, (int)B, x0, Xref, Uref, X, U, K, kff, iters, status, st); break;
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+    DTMPC_NA_CASES(CASE)
 #undef CASE
     default: return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
   }
@@ -431,7 +431,7 @@ static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B
   case n:                                                                                           \
     hipLaunchKernelGGL((tube_step_kernel<T, n>), grid_for(B), dim3(kBlock), 0, st, s, cn, cfn, cfa, a); \
     break;
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+    DTMPC_NA_CASES(CASE)
 #undef CASE
     default: return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
   }

@@ -122,7 +122,7 @@ static int launch_receding(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtm
   switch (cfg.nc) {
 #define CASE(n)                                                                                     \
   case n: hipLaunchKernelGGL((receding_kernel<T, n>), grid_for(B), dim3(kBlock), 0, st, s, c, cfg, a); break;
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+    DTMPC_NA_CASES(CASE)
 #undef CASE
     default: return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
   }

@@ -282,12 +282,12 @@ __device__ __forceinline__ T tape_cost(const DCost<T>& c, const Col<T>& X, const
     T r0, r1, r2, q0, q1;
     load_ref(c, Xr, rf, k, r0, r1, r2);
     load_uref(c, Ur, k, q0, q1);
-    J = J + stage_cost(c, X.at(k, 4, 0), X.at(k, 4, 1), X.at(k, 4, 2), X.at(k, 4, 3), U.at(k, 2, 0),
-                       U.at(k, 2, 1), r0, r1, r2, q0, q1);
+    J = J + stage_cost(c, T(X.at(k, 4, 0)), T(X.at(k, 4, 1)), T(X.at(k, 4, 2)), T(X.at(k, 4, 3)),
+                       T(U.at(k, 2, 0)), T(U.at(k, 2, 1)), r0, r1, r2, q0, q1);
   }
   T r0, r1, r2;
   load_ref(c, Xr, rf, N, r0, r1, r2);
-  return J + term_cost(c, X.at(N, 4, 0), X.at(N, 4, 1), X.at(N, 4, 2), X.at(N, 4, 3), r0, r1, r2);
+  return J + term_cost(c, T(X.at(N, 4, 0)), T(X.at(N, 4, 1)), T(X.at(N, 4, 2)), T(X.at(N, 4, 3)), r0, r1, r2);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -357,8 +357,8 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
   const int N = s.N;
   // V = clamp(V_init); X = rollout(x0, V)   (:127-131)
   for (int k = 0; k < N; ++k) {
-    U.at(k, 2, 0) = clampv(U.at(k, 2, 0), s.umin0, s.umax0);
-    U.at(k, 2, 1) = clampv(U.at(k, 2, 1), s.umin1, s.umax1);
+    U.at(k, 2, 0) = clampv(T(U.at(k, 2, 0)), s.umin0, s.umax0);
+    U.at(k, 2, 1) = clampv(T(U.at(k, 2, 1)), s.umin1, s.umax1);
   }
   rollout_traj(s, x0, X, U);
   T Bc0 = barrier_of_state(s, x0[0], x0[1]);
