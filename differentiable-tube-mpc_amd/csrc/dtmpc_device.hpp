@@ -133,6 +133,19 @@ struct Col {
   }
 };
 
+// Pin the first kFastObs obstacle entries of a kernel-local spec copy in VGPRs (an empty asm the
+// compiler cannot see through, so the values are neither re-loaded nor constant-folded back to
+// kernarg reads).  Used with DTMPC_OBS_REGS.
+template <typename T>
+__device__ __forceinline__ void obs_pin(DSpec<T>& s) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    __asm__ volatile("" : "+v"(s.cx[j]));
+    __asm__ volatile("" : "+v"(s.cy[j]));
+    __asm__ volatile("" : "+v"(s.r2[j]));
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // safety function h  (core/systems/dubins_obstacles.py)
 
@@ -145,9 +158,37 @@ __device__ __forceinline__ const DSpec<T>& kspec() {
   return *(const DSpec<T>*)(__builtin_amdgcn_kernarg_segment_ptr());  // addrspace(4) -> generic
 }
 
+// h_circle_k: runtime obstacle index, table read from the kernarg segment.
 template <typename T>
-__device__ __forceinline__ T h_circle(const DSpec<T>&, int i, T px, T py) {  // :16-30
+__device__ __forceinline__ T h_circle_k(int i, T px, T py) {  // :16-30
   const DSpec<T>& k = kspec<T>();
+  T dx = px - k.cx[i];
+  T dy = py - k.cy[i];
+  return dx * dx + dy * dy - k.r2[i];
+}
+
+// Obstacle table used by the compile-time-indexed paths: the spec the caller passes (DTMPC_OBS_REGS,
+// default).  The tube-step kernel passes a local spec whose first kFastObs table entries were pinned
+// in VGPRs at kernel start (obs_pin), so its unrolled obstacle loops read registers instead of
+// re-issuing scalar kernarg loads inside the step loops once SGPRs run short (tube step 7.51 ->
+// 7.33 ms).  -DDTMPC_OBS_KERNARG reads the kernarg segment everywhere.
+#ifndef DTMPC_OBS_KERNARG
+#define DTMPC_OBS_REGS 1
+#endif
+template <typename T>
+__device__ __forceinline__ const DSpec<T>& obs_tab(const DSpec<T>& s) {
+#ifdef DTMPC_OBS_REGS
+  return s;
+#else
+  (void)s;
+  return kspec<T>();
+#endif
+}
+
+// h_circle: compile-time obstacle index (unrolled loops only)
+template <typename T>
+__device__ __forceinline__ T h_circle(const DSpec<T>& s, int i, T px, T py) {  // :16-30
+  const DSpec<T>& k = obs_tab(s);
   T dx = px - k.cx[i];
   T dy = py - k.cy[i];
   return dx * dx + dy * dy - k.r2[i];
@@ -249,10 +290,10 @@ __device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* p
     // max_i fl(-beta h_i) == fl(-beta min_i h_i) (rounding is monotone): one v_min per obstacle
     T zmax[W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) zmax[w] = h_circle(s, 0, px[w], py[w]);
+    for (int w = 0; w < W; ++w) zmax[w] = h_circle_k<T>(0, px[w], py[w]);
     for (int i = 1; i < s.M; ++i) {
 #pragma unroll
-      for (int w = 0; w < W; ++w) zmax[w] = m_min(zmax[w], h_circle(s, i, px[w], py[w]));
+      for (int w = 0; w < W; ++w) zmax[w] = m_min(zmax[w], h_circle_k<T>(i, px[w], py[w]));
     }
 #pragma unroll
     for (int w = 0; w < W; ++w) zmax[w] = s.neg_beta * zmax[w];
@@ -261,7 +302,7 @@ __device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* p
     for (int w = 0; w < W; ++w) se[w] = T(0);
     for (int i = 0; i < s.M; ++i) {
 #pragma unroll
-      for (int w = 0; w < W; ++w) se[w] += m_exp(s.neg_beta * h_circle(s, i, px[w], py[w]) - zmax[w]);
+      for (int w = 0; w < W; ++w) se[w] += m_exp(s.neg_beta * h_circle_k<T>(i, px[w], py[w]) - zmax[w]);
     }
 #pragma unroll
     for (int w = 0; w < W; ++w) h[w] = s.neg_inv_beta * (zmax[w] + m_log(se[w]));
@@ -305,8 +346,8 @@ __device__ __forceinline__ T h_grad_fixed(const DSpec<T>& s, T px, T py, T& gx, 
   for (int i = 0; i < MO; ++i) {
     T e = m_exp(z[i] - zmax);
     se += e;
-    sx += e * (T(2) * (px - kspec<T>().cx[i]));
-    sy += e * (T(2) * (py - kspec<T>().cy[i]));
+    sx += e * (T(2) * (px - obs_tab(s).cx[i]));
+    sy += e * (T(2) * (py - obs_tab(s).cy[i]));
   }
   T inv = m_rcp(se);
   gx = sx * inv;
@@ -329,14 +370,14 @@ __device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy)
     }
   }
   if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0) {
-    T zmax = s.neg_beta * h_circle(s, 0, px, py);
+    T zmax = s.neg_beta * h_circle_k<T>(0, px, py);
     for (int i = 1; i < s.M; ++i) {
-      T z = s.neg_beta * h_circle(s, i, px, py);
+      T z = s.neg_beta * h_circle_k<T>(i, px, py);
       zmax = z > zmax ? z : zmax;
     }
     T se = T(0), sx = T(0), sy = T(0);
     for (int i = 0; i < s.M; ++i) {
-      T e = m_exp(s.neg_beta * h_circle(s, i, px, py) - zmax);
+      T e = m_exp(s.neg_beta * h_circle_k<T>(i, px, py) - zmax);
       se += e;
       sx += e * (T(2) * (px - kspec<T>().cx[i]));
       sy += e * (T(2) * (py - kspec<T>().cy[i]));

@@ -196,14 +196,30 @@ struct TubeArgs {
 };
 
 
+// kTubeLPT lanes per trajectory (1 or 2).  At the benchmark batch (65,536 trajectories) one lane per
+// trajectory is exactly one wave per SIMD and nothing hides latency; with 2 (paired line search,
+// line_search_pair) there are two waves per SIMD, each rolling out half the line-search candidates,
+// the rest of the step computed identically by both lanes of a pair (identical values stored twice).
+// Measured at B = 65,536: 2 lanes 8.27 ms vs 1 lane 7.54 ms (the 256-register cap of two waves per
+// SIMD spills 46 VGPRs to scratch, and the duplicated backward / commit work outweighs the overlap),
+// so the default is 1; the paired path stays parity-tested as a build option.
+#ifndef DTMPC_TUBE_LPT
+#define DTMPC_TUBE_LPT 1
+#endif
+constexpr int kTubeLPT = DTMPC_TUBE_LPT;
+
 template <typename T, int NA>
-__global__ void __launch_bounds__(kBlock) tube_step_kernel(DSpec<T> s, DCost<T> cn,
-                                                           DIlqr<T> cfn, DIlqr<T> cfa,
-                                                           TubeArgs<T> a) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kTubeLPT, kTubeLPT)))
+tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeArgs<T> a) {
   __shared__ T red[kBlock / 64][8];
+  DSpec<T> s = s_arg;
+#ifdef DTMPC_OBS_REGS
+  obs_pin(s);  // obstacle table in VGPRs for the whole step (obs_tab)
+#endif
   const int B = a.B;
   const int N = s.N;
-  int i = blockIdx.x * kBlock + threadIdx.x;
+  const int gl = blockIdx.x * kBlock + threadIdx.x;
+  const int i = gl / kTubeLPT, hl = gl % kTubeLPT;
   T acc[7] = {T(0), T(0), T(0), T(0), T(0), T(0), T(0)};
   if (i < B) {
     const size_t nb = (size_t)B;
@@ -219,7 +235,7 @@ __global__ void __launch_bounds__(kBlock) tube_step_kernel(DSpec<T> s, DCost<T> 
     Col<T> none = col<T>((void*)nullptr, i, B);
     Prof pr;
     pr.start();
-    st |= ilqr_traj<T, NA>(s, cn, cfn, xn0, Xn, Un, K, kf, none, 0, none, itn, pr, 0);
+    st |= ilqr_traj<T, NA, kTubeLPT>(s, cn, cfn, xn0, Xn, Un, K, kf, none, 0, none, itn, pr, 0, hl);
     // ancillary MPC tracking the nominal plan :863-909 (terminal weight Qa, :885, :891)
     DCost<T> ca;
     ca.kind = DTMPC_COST_TRACK;
@@ -233,7 +249,7 @@ __global__ void __launch_bounds__(kBlock) tube_step_kernel(DSpec<T> s, DCost<T> 
     ca.t0 = ca.t1 = ca.t2 = T(0);
     T xa0[4] = {x0, x1, x2, xb};
     pr.mark(8);
-    st |= ilqr_traj<T, NA>(s, ca, cfa, xa0, Xa, Ua, K, kf, Xn, 4, Un, ita, pr, 4);
+    st |= ilqr_traj<T, NA, kTubeLPT>(s, ca, cfa, xa0, Xa, Ua, K, kf, Xn, 4, Un, ita, pr, 4, hl);
     pr.mark(8);
     // upper loss, DOC sensitivity and analytic gradient :915-976
     st |= sens_traj<T, false, false, true>(s, ca, Xa, Ua, Xn, 4, Un, Xn, 4, K, kf, AB, none, none,
@@ -297,7 +313,7 @@ __global__ void __launch_bounds__(kBlock) tube_step_kernel(DSpec<T> s, DCost<T> 
       Ua.at(k, 2, 0) = Ua.at(k + 1, 2, 0);
       Ua.at(k, 2, 1) = Ua.at(k + 1, 2, 1);
     }
-    if (st) {
+    if (st || hl != 0) {  // a failed trajectory contributes nothing; a pair counts once
 #pragma unroll
       for (int j = 0; j < 7; ++j) acc[j] = T(0);
     }
@@ -429,7 +445,7 @@ static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B
   switch (cfn.nc) {
 #define CASE(n)                                                                                     \
   case n:                                                                                           \
-    hipLaunchKernelGGL((tube_step_kernel<T, n>), grid_for(B), dim3(kBlock), 0, st, s, cn, cfn, cfa, a); \
+    hipLaunchKernelGGL((tube_step_kernel<T, n>), grid_for(B * kTubeLPT), dim3(kBlock), 0, st, s, cn, cfn, cfa, a); \
     break;
     DTMPC_NA_CASES(CASE)
 #undef CASE
@@ -588,7 +604,7 @@ size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
   return el * (size_t)horizon * 20 * (size_t)B;
 }
 
-int64_t dtmpc_tube_partials_count(int64_t B) { return (B + kBlock - 1) / kBlock; }
+int64_t dtmpc_tube_partials_count(int64_t B) { return (B * kTubeLPT + kBlock - 1) / kBlock; }
 
 int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B,
                     int64_t global_offset, int64_t step, const dtmpc_tube_state* state,

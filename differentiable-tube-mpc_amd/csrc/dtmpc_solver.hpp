@@ -54,6 +54,17 @@ __device__ __forceinline__ void load_uref(const DCost<T>& c, const Col<T>& Ur, i
 #endif
 constexpr int kPrefetch = DTMPC_PREFETCH;
 
+// The backward pass and the commit rollout load their step inputs kRing steps ahead into a RING of
+// kRing register buffers that rotates by unrolling the step loop kRing times -- never by copying:
+// q[j] = q[j + 1] on a buffer whose load is still in flight makes the copy wait for that load, which
+// caps the shift-register form's effective distance at one step whatever its depth.  A step of
+// either pass (1,500-3,000 cycles) already outlasts an HBM miss (~900 cycles idle), and deeper rings
+// only add registers: the default is 1.
+#ifndef DTMPC_RING
+#define DTMPC_RING 1  // measured: ring depth 2 / 3 / 4 = +1 % / +2 % / +8 % tube-step time
+#endif
+constexpr int kRing = DTMPC_RING;
+
 // Everything the backward pass reads at step k: tape X[k], V[k] and the tracking references.
 template <typename T>
 struct BackIn {
@@ -103,46 +114,49 @@ __device__ __forceinline__ bool ilqr_backward(const DSpec<T>& s, const DCost<T>&
   T hn = h_grad(s, xn0, xn1, gxn, gyn);
   T dBn = dbarrier_relaxed(s, hn);
   bool ok = finite(R.Vx[0]) && finite(R.Vx[1]) && finite(R.Vx[2]) && finite(R.Vx[3]);
-  // step inputs (x_k, u_k, references) prefetched kPrefetch steps ahead of the recursion
-  BackIn<T> q[kPrefetch];
+  // step inputs (x_k, u_k, references) in a kRing-deep prefetch ring
+  BackIn<T> q[kRing];
 #pragma unroll
-  for (int j = 0; j < kPrefetch; ++j)
+  for (int j = 0; j < kRing; ++j)
     if (N - 1 - j >= 0) load_back(q[j], c, X, U, Xr, rf, Ur, N - 1 - j);
-  for (int k = N - 1; k >= 0; --k) {
-    const BackIn<T> cur = q[0];
+  for (int k0 = N - 1; k0 >= 0; k0 -= kRing) {
 #pragma unroll
-    for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
-    if (k - kPrefetch >= 0) load_back(q[kPrefetch - 1], c, X, U, Xr, rf, Ur, k - kPrefetch);
-    const T x0 = cur.X0, x1 = cur.X1, x2 = cur.X2, xb = cur.X3, u0 = cur.V0, u1 = cur.V1, q0 = cur.q0,
-            q1 = cur.q1;
-    r0 = cur.r0;
-    r1 = cur.r1;
-    r2 = cur.r2;
-    T sn, cs;
-    m_sincos(x2, &sn, &cs);
-    T gxk, gyk;
-    T hk = h_grad(s, x0, x1, gxk, gyk);
-    T dBk = dbarrier_relaxed(s, hk);
-    Jac<T> J = make_jac(s, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
-    deriv_dx(c, x0, x1, x2, r0, r1, r2, d0, d1, d2);
-    T lx[4] = {lxx[0] * d0, lxx[1] * d1, lxx[2] * d2, lxx[3] * xb};
-    T lu[2];
-    if (c.kind == DTMPC_COST_TRACK) {
-      lu[0] = luu[0] * (u0 - q0);
-      lu[1] = luu[1] * (u1 - q1);
-    } else {
-      lu[0] = luu[0] * u0;
-      lu[1] = luu[1] * u1;
+    for (int jr = 0; jr < kRing; ++jr) {
+      const int k = k0 - jr;
+      if (k < 0) break;
+      const BackIn<T> cur = q[jr];
+      if (k - kRing >= 0) load_back(q[jr], c, X, U, Xr, rf, Ur, k - kRing);
+      const T x0 = cur.X0, x1 = cur.X1, x2 = cur.X2, xb = cur.X3, u0 = cur.V0, u1 = cur.V1, q0 = cur.q0,
+              q1 = cur.q1;
+      r0 = cur.r0;
+      r1 = cur.r1;
+      r2 = cur.r2;
+      T sn, cs;
+      m_sincos(x2, &sn, &cs);
+      T gxk, gyk;
+      T hk = h_grad(s, x0, x1, gxk, gyk);
+      T dBk = dbarrier_relaxed(s, hk);
+      Jac<T> J = make_jac(s, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
+      deriv_dx(c, x0, x1, x2, r0, r1, r2, d0, d1, d2);
+      T lx[4] = {lxx[0] * d0, lxx[1] * d1, lxx[2] * d2, lxx[3] * xb};
+      T lu[2];
+      if (c.kind == DTMPC_COST_TRACK) {
+        lu[0] = luu[0] * (u0 - q0);
+        lu[1] = luu[1] * (u1 - q1);
+      } else {
+        lu[0] = luu[0] * u0;
+        lu[1] = luu[1] * u1;
+      }
+      T Kk[8], kk[2];
+      ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) K.at(k, 8, j) = Kk[j];
+      kf.at(k, 2, 0) = kk[0];
+      kf.at(k, 2, 1) = kk[1];
+      gxn = gxk;
+      gyn = gyk;
+      dBn = dBk;
     }
-    T Kk[8], kk[2];
-    ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) K.at(k, 8, j) = Kk[j];
-    kf.at(k, 2, 0) = kk[0];
-    kf.at(k, 2, 1) = kk[1];
-    gxn = gxk;
-    gyn = gyk;
-    dBn = dBk;
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) ok = ok && finite(R.Vx[i]);
@@ -272,6 +286,124 @@ __device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c,
   return ok ? best : -1;
 }
 
+// Paired line search: TWO lanes per trajectory (lane half h = 0, 1 of an adjacent lane pair), each
+// rolling out every other candidate -- candidate c = 2j + h (the last slot of half 1 repeats candidate
+// NC - 1 when NC is odd).  Both halves compute identical tapes everywhere else, so the only exchange
+// is here: the per-half first strict minimum (J, candidate) is combined with the partner's by
+// lexicographic (J, original position) order, which is exactly "strict <, first wins" over the
+// original list; the alpha = 0 rule and the finiteness flag are combined the same way.  Both halves
+// return the same decision.
+template <typename T, int NC>
+__device__ __forceinline__ int line_search_pair(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg,
+                                                const T* x0, T Bc0, const Col<T>& X, const Col<T>& U,
+                                                const Col<T>& K, const Col<T>& kf, const Col<T>& Xr, int rf,
+                                                const Col<T>& Ur, T Jprev, T& bestJ, T& al_out, int h) {
+  constexpr int NL = (NC + 1) / 2;
+  const int N = s.N;
+  T a0[NL], a1[NL], a2[NL], ab[NL], Bc[NL], J[NL], al[NL];
+  int ci[NL];
+#pragma unroll
+  for (int a = 0; a < NL; ++a) {
+    const int c0 = 2 * a, c1 = 2 * a + 1 < NC ? 2 * a + 1 : NC - 1;
+    ci[a] = h ? c1 : c0;
+    al[a] = h ? cfg.calphas[c1] : cfg.calphas[c0];
+    a0[a] = x0[0];
+    a1[a] = x0[1];
+    a2[a] = x0[2];
+    ab[a] = x0[3];
+    Bc[a] = Bc0;
+    J[a] = T(0);
+  }
+  StepIn<T> q[kPrefetch];
+#pragma unroll
+  for (int j = 0; j < kPrefetch; ++j)
+    if (j < N) load_step(q[j], c, X, U, K, kf, Xr, rf, Ur, j);
+  for (int k = 0; k < N; ++k) {
+    const StepIn<T> cur = q[0];
+#pragma unroll
+    for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
+    if (k + kPrefetch < N) load_step(q[kPrefetch - 1], c, X, U, K, kf, Xr, rf, Ur, k + kPrefetch);
+    T u0[NL], u1[NL];
+#pragma unroll
+    for (int a = 0; a < NL; ++a) {
+      T e0 = a0[a] - cur.X0, e1 = a1[a] - cur.X1, e2 = a2[a] - cur.X2, e3 = ab[a] - cur.X3;
+      T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
+      T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
+      u0[a] = clampv(cur.V0 + al[a] * du0, s.umin0, s.umax0);
+      u1[a] = clampv(cur.V1 + al[a] * du1, s.umin1, s.umax1);
+      J[a] = J[a] + stage_cost(c, a0[a], a1[a], a2[a], ab[a], u0[a], u1[a], cur.r0, cur.r1, cur.r2,
+                               cur.q0, cur.q1);
+    }
+    fhat_vec<T, NL>(s, a0, a1, a2, ab, u0, u1, Bc);
+  }
+  T r0, r1, r2;
+  load_ref(c, Xr, rf, N, r0, r1, r2);
+  bool ok = true;
+#pragma unroll
+  for (int a = 0; a < NL; ++a) {
+    J[a] = J[a] + term_cost(c, a0[a], a1[a], a2[a], ab[a], r0, r1, r2);
+    ok = ok && finite(J[a]);
+  }
+  // this half's first strict minimum (its candidates are in increasing original order)
+  T bJ = J[0];
+  int bi = ci[0];
+#pragma unroll
+  for (int a = 1; a < NL; ++a) {
+    if (J[a] < bJ) {
+      bJ = J[a];
+      bi = ci[a];
+    }
+  }
+  // the zero candidate's neighbours: min over candidates before / after position zpos
+  T mb = T(0), ma = T(0);
+  int hb = 0, ha = 0;
+  if (cfg.zpos >= 0) {
+#pragma unroll
+    for (int a = 0; a < NL; ++a) {
+      if (cfg.cpos[ci[a]] < cfg.zpos) {
+        mb = (!hb || J[a] < mb) ? J[a] : mb;
+        hb = 1;
+      } else {
+        ma = (!ha || J[a] < ma) ? J[a] : ma;
+        ha = 1;
+      }
+    }
+  }
+  // combine with the partner lane
+  const T oJ = __shfl_xor(bJ, 1, 64);
+  const int oi = __shfl_xor(bi, 1, 64);
+  ok = __shfl_xor((int)ok, 1, 64) && ok;
+  if (oJ < bJ || (oJ == bJ && oi < bi)) {
+    bJ = oJ;
+    bi = oi;
+  }
+  bestJ = bJ;
+  int best = cfg.cpos[0];
+  al_out = cfg.calphas[0];
+#pragma unroll
+  for (int cc = 1; cc < NC; ++cc) {
+    if (bi == cc) {
+      best = cfg.cpos[cc];
+      al_out = cfg.calphas[cc];
+    }
+  }
+  if (cfg.zpos >= 0) {
+    const T omb = __shfl_xor(mb, 1, 64), oma = __shfl_xor(ma, 1, 64);
+    const int ohb = __shfl_xor(hb, 1, 64), oha = __shfl_xor(ha, 1, 64);
+    if (ohb) mb = (!hb || omb < mb) ? omb : mb;
+    if (oha) ma = (!ha || oma < ma) ? oma : ma;
+    hb |= ohb;
+    ha |= oha;
+    if ((!hb || Jprev < mb) && (!ha || Jprev <= ma)) {
+      best = cfg.zpos;
+      bestJ = Jprev;
+      al_out = T(0);
+    }
+    ok = ok && finite(Jprev);
+  }
+  return ok ? best : -1;
+}
+
 // cost of the tape (X, U) with the line search's accumulation order: the alpha = 0 candidate's cost
 // before the first iteration (core/ddp.py:256-301 rolls it out; it is the initial tape)
 template <typename T>
@@ -301,28 +433,31 @@ __device__ __forceinline__ void commit_candidate(const DSpec<T>& s, T al, const 
   DCost<T> none;
   none.kind = DTMPC_COST_TARGET;  // the references are not needed here
   Col<T> nc = X;
-  StepIn<T> q[kPrefetch];
+  StepIn<T> q[kRing];
 #pragma unroll
-  for (int j = 0; j < kPrefetch; ++j)
+  for (int j = 0; j < kRing; ++j)
     if (j < N) load_step(q[j], none, X, U, K, kf, nc, 0, nc, j);
-  for (int k = 0; k < N; ++k) {
-    // the prefetch also fetches the OLD X[k+j] before step k+j-1 overwrites it
-    const StepIn<T> cur = q[0];
+  for (int k0 = 0; k0 < N; k0 += kRing) {
 #pragma unroll
-    for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
-    if (k + kPrefetch < N) load_step(q[kPrefetch - 1], none, X, U, K, kf, nc, 0, nc, k + kPrefetch);
-    T e0 = s0[0] - cur.X0, e1 = s1[0] - cur.X1, e2 = s2[0] - cur.X2, e3 = sb[0] - cur.X3;
-    T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
-    T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
-    T u0[1] = {clampv(cur.V0 + al * du0, s.umin0, s.umax0)};
-    T u1[1] = {clampv(cur.V1 + al * du1, s.umin1, s.umax1)};
-    U.at(k, 2, 0) = u0[0];
-    U.at(k, 2, 1) = u1[0];
-    fhat_vec<T, 1>(s, s0, s1, s2, sb, u0, u1, Bc);
-    X.at(k + 1, 4, 0) = s0[0];
-    X.at(k + 1, 4, 1) = s1[0];
-    X.at(k + 1, 4, 2) = s2[0];
-    X.at(k + 1, 4, 3) = sb[0];
+    for (int jr = 0; jr < kRing; ++jr) {
+      const int k = k0 + jr;
+      if (k >= N) break;
+      // the ring also fetches the OLD X[k+kRing] before step k+kRing-1 overwrites it
+      const StepIn<T> cur = q[jr];
+      if (k + kRing < N) load_step(q[jr], none, X, U, K, kf, nc, 0, nc, k + kRing);
+      T e0 = s0[0] - cur.X0, e1 = s1[0] - cur.X1, e2 = s2[0] - cur.X2, e3 = sb[0] - cur.X3;
+      T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
+      T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
+      T u0[1] = {clampv(cur.V0 + al * du0, s.umin0, s.umax0)};
+      T u1[1] = {clampv(cur.V1 + al * du1, s.umin1, s.umax1)};
+      U.at(k, 2, 0) = u0[0];
+      U.at(k, 2, 1) = u1[0];
+      fhat_vec<T, 1>(s, s0, s1, s2, sb, u0, u1, Bc);
+      X.at(k + 1, 4, 0) = s0[0];
+      X.at(k + 1, 4, 1) = s1[0];
+      X.at(k + 1, 4, 2) = s2[0];
+      X.at(k + 1, 4, 3) = sb[0];
+    }
   }
 }
 
@@ -349,11 +484,11 @@ __device__ __forceinline__ void rollout_traj(const DSpec<T>& s, const T* x0, con
 // ---------------------------------------------------------------------------------------------
 // iLQR for one trajectory (core/ddp.py:102-307).  U: in V_init, out V*.  X: out X*.
 // K/kf: scratch + gains of the last backward pass.  Returns DTMPC_ST_* bits.
-template <typename T, int NA>
+template <typename T, int NA, int LPT = 1>
 __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, const T* x0,
                          const Col<T>& X, const Col<T>& U, const Col<T>& K, const Col<T>& kf,
                          const Col<T>& Xr, int rf, const Col<T>& Ur, int& iters, Prof& pr,
-                         int pb) {
+                         int pb, int h = 0) {
   const int N = s.N;
   // V = clamp(V_init); X = rollout(x0, V)   (:127-131)
   for (int k = 0; k < N; ++k) {
@@ -373,7 +508,11 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
     if (!ilqr_backward(s, c, cfg.reg, X, U, K, kf, Xr, rf, Ur)) return DTMPC_ST_NONFINITE;
     pr.mark(pb + 1);
     T bestJ, al;
-    int best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, K, kf, Xr, rf, Ur, Jcur, bestJ, al);
+    int best;
+    if constexpr (LPT == 2)
+      best = line_search_pair<T, NA>(s, c, cfg, x0, Bc0, X, U, K, kf, Xr, rf, Ur, Jcur, bestJ, al, h);
+    else
+      best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, K, kf, Xr, rf, Ur, Jcur, bestJ, al);
     pr.mark(pb + 2);
     if (best < 0) return DTMPC_ST_NONFINITE;
     if (al != T(0)) commit_candidate(s, al, x0, Bc0, X, U, K, kf);
