@@ -150,10 +150,10 @@ __global__ void __launch_bounds__(kBlock) general_step_kernel(DSpec<T> s, DIlqr<
     Prof pr;
     // nominal MPC with theta-bar (:217-291)
     T xn0[4] = {a.xbar[i], a.xbar[nb + i], a.xbar[2 * nb + i], a.bbar[i]};
-    st |= ilqr_traj<T, NA>(sn, cn, cfn, xn0, Xn, Un, K, kf, none, 0, none, itn, pr, 0);
+    st |= ilqr_traj<T, NA>(sn, cn, cfn, xn0, Xn, Un, GainsSoA<T>{K, kf}, none, 0, none, itn, pr, 0);
     // ancillary MPC with theta tracking the nominal plan (:296-392)
     T xa0[4] = {a.x[i], a.x[nb + i], a.x[2 * nb + i], a.b[i]};
-    st |= ilqr_traj<T, NA>(sa, ca, cfa, xa0, Xa, Ua, K, kf, Xn, 4, Un, ita, pr, 4);
+    st |= ilqr_traj<T, NA>(sa, ca, cfa, xa0, Xa, Ua, GainsSoA<T>{K, kf}, Xn, 4, Un, ita, pr, 4);
     // upper loss L = ||x* - xbar||^2 + ||b*||^2 (:403-408)
     T L1 = T(0), L2 = T(0);
     for (int k = 0; k <= N; ++k) {

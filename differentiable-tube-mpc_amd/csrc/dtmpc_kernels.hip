@@ -104,8 +104,9 @@ __global__ void __launch_bounds__(kBlock) ilqr_kernel(DSpec<T> s, DCost<T> c, DI
   int it = 0;
   Prof pr;
   pr.start();
-  int st = ilqr_traj<T, NA>(s, c, cfg, x0, col<T>(Xp, i, B), col<T>(Up, i, B), col<T>(Kp, i, B),
-                            col<T>(kfp, i, B), col<T>(Xrp, i, B), 3, col<T>(Urp, i, B), it, pr, 0);
+  int st = ilqr_traj<T, NA>(s, c, cfg, x0, col<T>(Xp, i, B), col<T>(Up, i, B),
+                            GainsSoA<T>{col<T>(Kp, i, B), col<T>(kfp, i, B)}, col<T>(Xrp, i, B), 3,
+                            col<T>(Urp, i, B), it, pr, 0);
   pr.flush();
   if (iters) iters[i] = it;
   if (status) status[i] |= st;
@@ -235,7 +236,12 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
     Col<T> none = col<T>((void*)nullptr, i, B);
     Prof pr;
     pr.start();
-    st |= ilqr_traj<T, NA, kTubeLPT>(s, cn, cfn, xn0, Xn, Un, K, kf, none, 0, none, itn, pr, 0, hl);
+    // the iLQR gains: per-lane contiguous (GainsAoS) in their own region of the workspace.  It must
+    // not overlap the sensitivity's SoA scratch (K / kf / AB above): an AoS block of lane i covers
+    // SoA cells of other lanes, which other waves may be writing in their sensitivity pass meanwhile.
+    const GainsAoS<T> gains{a.work + (size_t)N * 20 * nb, a.work + (size_t)N * 28 * nb, (unsigned)B,
+                            (unsigned)i};
+    st |= ilqr_traj<T, NA, kTubeLPT>(s, cn, cfn, xn0, Xn, Un, gains, none, 0, none, itn, pr, 0, hl);
     // ancillary MPC tracking the nominal plan :863-909 (terminal weight Qa, :885, :891)
     DCost<T> ca;
     ca.kind = DTMPC_COST_TRACK;
@@ -249,7 +255,7 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
     ca.t0 = ca.t1 = ca.t2 = T(0);
     T xa0[4] = {x0, x1, x2, xb};
     pr.mark(8);
-    st |= ilqr_traj<T, NA, kTubeLPT>(s, ca, cfa, xa0, Xa, Ua, K, kf, Xn, 4, Un, ita, pr, 4, hl);
+    st |= ilqr_traj<T, NA, kTubeLPT>(s, ca, cfa, xa0, Xa, Ua, gains, Xn, 4, Un, ita, pr, 4, hl);
     pr.mark(8);
     // upper loss, DOC sensitivity and analytic gradient :915-976
     st |= sens_traj<T, false, false, true>(s, ca, Xa, Ua, Xn, 4, Un, Xn, 4, K, kf, AB, none, none,
@@ -601,7 +607,7 @@ int dtmpc_doc_grad(int dtype, int32_t horizon, int64_t B, const void* Xaux, cons
 
 size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
   size_t el = dtype == DTMPC_F64 ? 8 : 4;
-  return el * (size_t)horizon * 20 * (size_t)B;
+  return el * (size_t)horizon * 30 * (size_t)B;  // sensitivity K / kf / AB (SoA, 20) + iLQR gains (AoS, 10)
 }
 
 int64_t dtmpc_tube_partials_count(int64_t B) { return (B * kTubeLPT + kBlock - 1) / kBlock; }

@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(kBlock) receding_kernel(DSpec<T> s, DCost<T> c
   Prof pr;
   for (int t = 0; t < a.H; ++t) {
     int it = 0;
-    st |= ilqr_traj<T, NA>(s, c, cfg, x, X, U, K, kf, none, 0, none, it, pr, 0);
+    st |= ilqr_traj<T, NA>(s, c, cfg, x, X, U, GainsSoA<T>{K, kf}, none, 0, none, it, pr, 0);
     T u0[1] = {U.at(0, 2, 0)}, u1[1] = {U.at(0, 2, 1)};
     lg.at(t, 6, 0) = x[0];
     lg.at(t, 6, 1) = x[1];

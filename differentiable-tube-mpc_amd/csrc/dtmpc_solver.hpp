@@ -23,6 +23,76 @@ __device__ __forceinline__ void cost_diag(const DCost<T>& c, T* lxx, T* luu, T* 
   pxx[3] = T(2) * c.qb;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Feedback gains K [N][2x4] and k [N][2] of the last backward pass, written by the backward pass and
+// read by the line search and the commit.  Two layouts:
+//   GainsSoA  -- planes [N][8][B] / [N][2][B] (the ABI layout of dtmpc_ilqr_solve's K_out / k_out);
+//   GainsAoS  -- per step, each lane's 8 + 2 values contiguous ([N][B][8] / [N][B][2]): two 16-B and
+//                one 8-B access per step instead of ten 4-B ones, and a wave's gains of one step in
+//                one 2 KB + 512 B span instead of ten planes 4*B bytes apart.  Used for the tube
+//                step's internal workspace (the ten-plane stores were the costliest part of the
+//                backward pass: without them the tube step ran 16 % faster).
+template <typename T>
+struct GainsSoA {
+  Col<T> K, kf;
+  __device__ __forceinline__ void store(int k, const T* Kk, const T* kk) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) K.at(k, 8, j) = Kk[j];
+    kf.at(k, 2, 0) = kk[0];
+    kf.at(k, 2, 1) = kk[1];
+  }
+  __device__ __forceinline__ void load(int k, T* Kk, T& k0, T& k1) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Kk[j] = K.at(k, 8, j);
+    k0 = kf.at(k, 2, 0);
+    k1 = kf.at(k, 2, 1);
+  }
+};
+
+template <typename T>
+struct GainsAoS {
+  typedef T v2 __attribute__((ext_vector_type(2)));
+  typedef T v4 __attribute__((ext_vector_type(4)));
+  T* Kb;  // [N][B][8]
+  T* kb;  // [N][B][2]
+  unsigned ld, lane;
+  __device__ __forceinline__ T* kp(int k) const {
+    return (T*)__builtin_assume_aligned(Kb + ((size_t)(unsigned)k * ld + lane) * 8, 16);
+  }
+  __device__ __forceinline__ T* fp(int k) const {
+    return (T*)__builtin_assume_aligned(kb + ((size_t)(unsigned)k * ld + lane) * 2, 8);
+  }
+  __device__ __forceinline__ void store(int k, const T* Kk, const T* kk) const {
+    T* p = kp(k);
+    if constexpr (sizeof(T) == 4) {
+      *(v4*)p = v4{Kk[0], Kk[1], Kk[2], Kk[3]};
+      *(v4*)(p + 4) = v4{Kk[4], Kk[5], Kk[6], Kk[7]};
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) *(v2*)(p + j) = v2{Kk[j], Kk[j + 1]};
+    }
+    *(v2*)fp(k) = v2{kk[0], kk[1]};
+  }
+  __device__ __forceinline__ void load(int k, T* Kk, T& k0, T& k1) const {
+    const T* p = kp(k);
+    if constexpr (sizeof(T) == 4) {
+      v4 a = *(const v4*)p, b = *(const v4*)(p + 4);
+      Kk[0] = a.x; Kk[1] = a.y; Kk[2] = a.z; Kk[3] = a.w;
+      Kk[4] = b.x; Kk[5] = b.y; Kk[6] = b.z; Kk[7] = b.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        v2 a = *(const v2*)(p + j);
+        Kk[j] = a.x;
+        Kk[j + 1] = a.y;
+      }
+    }
+    v2 f = *(const v2*)fp(k);
+    k0 = f.x;
+    k1 = f.y;
+  }
+};
+
 template <typename T>
 __device__ __forceinline__ void load_ref(const DCost<T>& c, const Col<T>& Xr, int rf, int k, T& r0,
                                          T& r1, T& r2) {
@@ -89,9 +159,9 @@ __device__ __forceinline__ void load_back(BackIn<T>& L, const DCost<T>& c, const
 // backward pass (core/ddp.py:172-254): linearise along (X, U) and run the Riccati recursion,
 // writing K [N][8], kff [N][2].  grad h / B' at x_{k+1} are carried from step k+1 (the reference
 // recomputes x_{k+1} = f(x_k, u_k) inside dubins_augmented_jacobian; it is the tape's X[k+1]).
-template <typename T>
+template <typename T, typename G>
 __device__ __forceinline__ bool ilqr_backward(const DSpec<T>& s, const DCost<T>& c, T reg, const Col<T>& X,
-                              const Col<T>& U, const Col<T>& K, const Col<T>& kf,
+                              const Col<T>& U, const G& gains,
                               const Col<T>& Xr, int rf, const Col<T>& Ur) {
   const int N = s.N;
   T lxx[4], luu[2], pxx[4];
@@ -149,10 +219,7 @@ __device__ __forceinline__ bool ilqr_backward(const DSpec<T>& s, const DCost<T>&
       }
       T Kk[8], kk[2];
       ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) K.at(k, 8, j) = Kk[j];
-      kf.at(k, 2, 0) = kk[0];
-      kf.at(k, 2, 1) = kk[1];
+      gains.store(k, Kk, kk);
       gxn = gxk;
       gyn = gyk;
       dBn = dBk;
@@ -172,9 +239,9 @@ struct StepIn {
   T X0, X1, X2, X3, V0, V1, K[8], k0, k1, r0, r1, r2, q0, q1;
 };
 
-template <typename T>
+template <typename T, typename G>
 __device__ __forceinline__ void load_step(StepIn<T>& L, const DCost<T>& c, const Col<T>& X,
-                                          const Col<T>& U, const Col<T>& K, const Col<T>& kf,
+                                          const Col<T>& U, const G& gains,
                                           const Col<T>& Xr, int rf, const Col<T>& Ur, int k) {
   L.X0 = X.at(k, 4, 0);
   L.X1 = X.at(k, 4, 1);
@@ -182,10 +249,7 @@ __device__ __forceinline__ void load_step(StepIn<T>& L, const DCost<T>& c, const
   L.X3 = X.at(k, 4, 3);
   L.V0 = U.at(k, 2, 0);
   L.V1 = U.at(k, 2, 1);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) L.K[j] = K.at(k, 8, j);
-  L.k0 = kf.at(k, 2, 0);
-  L.k1 = kf.at(k, 2, 1);
+  gains.load(k, L.K, L.k0, L.k1);
   load_ref(c, Xr, rf, k, L.r0, L.r1, L.r2);
   load_uref(c, Ur, k, L.q0, L.q1);
 }
@@ -195,10 +259,10 @@ __device__ __forceinline__ void load_step(StepIn<T>& L, const DCost<T>& c, const
 // the alpha = 0 candidate (cfg.zpos) has cost Jprev (the current tape).  Returns the ORIGINAL index
 // of the strictly smallest cost (first wins ties), with its alpha in al_out, or -1 if any candidate is
 // non-finite.
-template <typename T, int NC>
+template <typename T, int NC, typename G>
 __device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg,
                                            const T* x0, T Bc0, const Col<T>& X, const Col<T>& U,
-                                           const Col<T>& K, const Col<T>& kf, const Col<T>& Xr, int rf,
+                                           const G& gains, const Col<T>& Xr, int rf,
                                            const Col<T>& Ur, T Jprev, T& bestJ, T& al_out) {
   const int N = s.N;
   T a0[NC], a1[NC], a2[NC], ab[NC], Bc[NC], J[NC];
@@ -214,12 +278,12 @@ __device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c,
   StepIn<T> q[kPrefetch];
 #pragma unroll
   for (int j = 0; j < kPrefetch; ++j)
-    if (j < N) load_step(q[j], c, X, U, K, kf, Xr, rf, Ur, j);
+    if (j < N) load_step(q[j], c, X, U, gains, Xr, rf, Ur, j);
   for (int k = 0; k < N; ++k) {
     const StepIn<T> cur = q[0];
 #pragma unroll
     for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
-    if (k + kPrefetch < N) load_step(q[kPrefetch - 1], c, X, U, K, kf, Xr, rf, Ur, k + kPrefetch);
+    if (k + kPrefetch < N) load_step(q[kPrefetch - 1], c, X, U, gains, Xr, rf, Ur, k + kPrefetch);
     T u0[NC], u1[NC];
 #pragma unroll
     for (int a = 0; a < NC; ++a) {
@@ -293,10 +357,10 @@ __device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c,
 // lexicographic (J, original position) order, which is exactly "strict <, first wins" over the
 // original list; the alpha = 0 rule and the finiteness flag are combined the same way.  Both halves
 // return the same decision.
-template <typename T, int NC>
+template <typename T, int NC, typename G>
 __device__ __forceinline__ int line_search_pair(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg,
                                                 const T* x0, T Bc0, const Col<T>& X, const Col<T>& U,
-                                                const Col<T>& K, const Col<T>& kf, const Col<T>& Xr, int rf,
+                                                const G& gains, const Col<T>& Xr, int rf,
                                                 const Col<T>& Ur, T Jprev, T& bestJ, T& al_out, int h) {
   constexpr int NL = (NC + 1) / 2;
   const int N = s.N;
@@ -317,12 +381,12 @@ __device__ __forceinline__ int line_search_pair(const DSpec<T>& s, const DCost<T
   StepIn<T> q[kPrefetch];
 #pragma unroll
   for (int j = 0; j < kPrefetch; ++j)
-    if (j < N) load_step(q[j], c, X, U, K, kf, Xr, rf, Ur, j);
+    if (j < N) load_step(q[j], c, X, U, gains, Xr, rf, Ur, j);
   for (int k = 0; k < N; ++k) {
     const StepIn<T> cur = q[0];
 #pragma unroll
     for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
-    if (k + kPrefetch < N) load_step(q[kPrefetch - 1], c, X, U, K, kf, Xr, rf, Ur, k + kPrefetch);
+    if (k + kPrefetch < N) load_step(q[kPrefetch - 1], c, X, U, gains, Xr, rf, Ur, k + kPrefetch);
     T u0[NL], u1[NL];
 #pragma unroll
     for (int a = 0; a < NL; ++a) {
@@ -425,9 +489,9 @@ __device__ __forceinline__ T tape_cost(const DCost<T>& c, const Col<T>& X, const
 // ---------------------------------------------------------------------------------------------
 // Materialise the chosen candidate in place: X, U <- rollout with step alpha (same arithmetic
 // as the candidate lane of line_search).  X[k+1] of the old tape is read before it is replaced.
-template <typename T>
+template <typename T, typename G>
 __device__ __forceinline__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, const Col<T>& X,
-                                 const Col<T>& U, const Col<T>& K, const Col<T>& kf) {
+                                 const Col<T>& U, const G& gains) {
   const int N = s.N;
   T s0[1] = {x0[0]}, s1[1] = {x0[1]}, s2[1] = {x0[2]}, sb[1] = {x0[3]}, Bc[1] = {Bc0};
   DCost<T> none;
@@ -436,7 +500,7 @@ __device__ __forceinline__ void commit_candidate(const DSpec<T>& s, T al, const 
   StepIn<T> q[kRing];
 #pragma unroll
   for (int j = 0; j < kRing; ++j)
-    if (j < N) load_step(q[j], none, X, U, K, kf, nc, 0, nc, j);
+    if (j < N) load_step(q[j], none, X, U, gains, nc, 0, nc, j);
   for (int k0 = 0; k0 < N; k0 += kRing) {
 #pragma unroll
     for (int jr = 0; jr < kRing; ++jr) {
@@ -444,7 +508,7 @@ __device__ __forceinline__ void commit_candidate(const DSpec<T>& s, T al, const 
       if (k >= N) break;
       // the ring also fetches the OLD X[k+kRing] before step k+kRing-1 overwrites it
       const StepIn<T> cur = q[jr];
-      if (k + kRing < N) load_step(q[jr], none, X, U, K, kf, nc, 0, nc, k + kRing);
+      if (k + kRing < N) load_step(q[jr], none, X, U, gains, nc, 0, nc, k + kRing);
       T e0 = s0[0] - cur.X0, e1 = s1[0] - cur.X1, e2 = s2[0] - cur.X2, e3 = sb[0] - cur.X3;
       T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
       T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
@@ -484,9 +548,9 @@ __device__ __forceinline__ void rollout_traj(const DSpec<T>& s, const T* x0, con
 // ---------------------------------------------------------------------------------------------
 // iLQR for one trajectory (core/ddp.py:102-307).  U: in V_init, out V*.  X: out X*.
 // K/kf: scratch + gains of the last backward pass.  Returns DTMPC_ST_* bits.
-template <typename T, int NA, int LPT = 1>
+template <typename T, int NA, int LPT = 1, typename G = GainsSoA<T>>
 __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, const T* x0,
-                         const Col<T>& X, const Col<T>& U, const Col<T>& K, const Col<T>& kf,
+                         const Col<T>& X, const Col<T>& U, const G& gains,
                          const Col<T>& Xr, int rf, const Col<T>& Ur, int& iters, Prof& pr,
                          int pb, int h = 0) {
   const int N = s.N;
@@ -505,17 +569,17 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
   iters = 0;
   for (int it = 0; it < cfg.max_iter; ++it) {
     iters = it + 1;
-    if (!ilqr_backward(s, c, cfg.reg, X, U, K, kf, Xr, rf, Ur)) return DTMPC_ST_NONFINITE;
+    if (!ilqr_backward(s, c, cfg.reg, X, U, gains, Xr, rf, Ur)) return DTMPC_ST_NONFINITE;
     pr.mark(pb + 1);
     T bestJ, al;
     int best;
     if constexpr (LPT == 2)
-      best = line_search_pair<T, NA>(s, c, cfg, x0, Bc0, X, U, K, kf, Xr, rf, Ur, Jcur, bestJ, al, h);
+      best = line_search_pair<T, NA>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, Jcur, bestJ, al, h);
     else
-      best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, K, kf, Xr, rf, Ur, Jcur, bestJ, al);
+      best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, Jcur, bestJ, al);
     pr.mark(pb + 2);
     if (best < 0) return DTMPC_ST_NONFINITE;
-    if (al != T(0)) commit_candidate(s, al, x0, Bc0, X, U, K, kf);
+    if (al != T(0)) commit_candidate(s, al, x0, Bc0, X, U, gains);
     Jcur = bestJ;
     pr.mark(pb + 3);
     // :303-305

@@ -47,7 +47,7 @@ def main():
     N = 50
     Bc = 262144
     known_r, known_w = 4 * Bc * (4 + 2 * N), 4 * Bc * 4 * (N + 1)
-    res = {"kernel": "tube_step_kernel<float,7>", "batch": batch, "counters_per_dispatch": tube,
+    res = {"kernel": "tube_step_kernel<float, 6> (7 alphas: 6 rolled out + alpha = 0 from the current tape)", "batch": batch, "counters_per_dispatch": tube,
            "kernel_trace": kernel_stats(root, "tube_step_kernel")}
     if "FETCH_SIZE" in tube and "WRITE_SIZE" in tube:
         raw = 1024.0 * (tube["FETCH_SIZE"] + tube["WRITE_SIZE"])

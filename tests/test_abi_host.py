@@ -113,7 +113,7 @@ def test_arguments_validated_before_any_device_call(lib):
     state = _abi.DtmpcTubeState()
     rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
     assert rc == _abi.ERR_BAD_ARG and b"same width" in lib.dtmpc_last_error()
-    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536) == 4 * 50 * 20 * 65536
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536) == 4 * 50 * 30 * 65536  # SoA scratch 20 + AoS gains 10
     assert lib.dtmpc_tube_partials_count(65536) == 256
     assert lib.dtmpc_sensitivity_workspace_bytes(_abi.F64, 50, 10, 1) == 8 * 10 * (50 * 20 + 51 * 20)
 
