@@ -131,9 +131,13 @@ constexpr int kPrefetch = DTMPC_PREFETCH;
 // either pass (1,500-3,000 cycles) already outlasts an HBM miss (~900 cycles idle), and deeper rings
 // only add registers: the default is 1.
 #ifndef DTMPC_RING
-#define DTMPC_RING 1  // measured: ring depth 2 / 3 / 4 = +1 % / +2 % / +8 % tube-step time
+#define DTMPC_RING 1  // backward pass; measured (both passes): depth 2 / 3 / 4 = +1 / +2 / +8 % step time
+#endif
+#ifndef DTMPC_RING_COMMIT
+#define DTMPC_RING_COMMIT 3  // commit rollout; measured depth 1 / 2 / 3 / 4 = 7.12 / 7.06 / 7.02 / 7.03 ms
 #endif
 constexpr int kRing = DTMPC_RING;
+constexpr int kRingC = DTMPC_RING_COMMIT;
 
 // Everything the backward pass reads at step k: tape X[k], V[k] and the tracking references.
 template <typename T>
@@ -497,18 +501,18 @@ __device__ __forceinline__ void commit_candidate(const DSpec<T>& s, T al, const 
   DCost<T> none;
   none.kind = DTMPC_COST_TARGET;  // the references are not needed here
   Col<T> nc = X;
-  StepIn<T> q[kRing];
+  StepIn<T> q[kRingC];
 #pragma unroll
-  for (int j = 0; j < kRing; ++j)
+  for (int j = 0; j < kRingC; ++j)
     if (j < N) load_step(q[j], none, X, U, gains, nc, 0, nc, j);
-  for (int k0 = 0; k0 < N; k0 += kRing) {
+  for (int k0 = 0; k0 < N; k0 += kRingC) {
 #pragma unroll
-    for (int jr = 0; jr < kRing; ++jr) {
+    for (int jr = 0; jr < kRingC; ++jr) {
       const int k = k0 + jr;
       if (k >= N) break;
-      // the ring also fetches the OLD X[k+kRing] before step k+kRing-1 overwrites it
+      // the ring also fetches the OLD X[k+kRingC] before step k+kRingC-1 overwrites it
       const StepIn<T> cur = q[jr];
-      if (k + kRing < N) load_step(q[jr], none, X, U, gains, nc, 0, nc, k + kRing);
+      if (k + kRingC < N) load_step(q[jr], none, X, U, gains, nc, 0, nc, k + kRingC);
       T e0 = s0[0] - cur.X0, e1 = s1[0] - cur.X1, e2 = s2[0] - cur.X2, e3 = sb[0] - cur.X3;
       T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
       T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
@@ -570,6 +574,10 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
   for (int it = 0; it < cfg.max_iter; ++it) {
     iters = it + 1;
     if (!ilqr_backward(s, c, cfg.reg, X, U, gains, Xr, rf, Ur)) return DTMPC_ST_NONFINITE;
+#ifdef DTMPC_DIAG_BW2  // timing attribution only: the pass again (idempotent)
+    __asm__ volatile("" ::: "memory");
+    if (!ilqr_backward(s, c, cfg.reg, X, U, gains, Xr, rf, Ur)) return DTMPC_ST_NONFINITE;
+#endif
     pr.mark(pb + 1);
     T bestJ, al;
     int best;
@@ -577,9 +585,17 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
       best = line_search_pair<T, NA>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, Jcur, bestJ, al, h);
     else
       best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, Jcur, bestJ, al);
+#ifdef DTMPC_DIAG_LS2  // timing attribution only: the pass again (same decision)
+    __asm__ volatile("" ::: "memory");
+    best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, Jcur, bestJ, al);
+#endif
     pr.mark(pb + 2);
     if (best < 0) return DTMPC_ST_NONFINITE;
     if (al != T(0)) commit_candidate(s, al, x0, Bc0, X, U, gains);
+#ifdef DTMPC_DIAG_CM2  // timing attribution only: a second rollout (results change)
+    __asm__ volatile("" ::: "memory");
+    if (al != T(0)) commit_candidate(s, al, x0, Bc0, X, U, gains);
+#endif
     Jcur = bestJ;
     pr.mark(pb + 3);
     // :303-305
