@@ -17,6 +17,13 @@
 
 namespace dtmpc {
 
+// Forward-pass arithmetic (rollouts, line-search candidates, commit, costs, h, barriers) is
+// evaluated WITHOUT multiply-add contraction: every product and sum rounded as the reference's
+// PyTorch CPU code rounds it.  This makes the scalar and the packed-pair (dtmpc_ls_pk.hpp) forms
+// of a rollout bitwise identical by construction -- the committed tape is exactly the candidate the
+// line search priced -- instead of depending on where the compiler happens to fuse.
+#define DTMPC_NOCONTRACT _Pragma("clang fp contract(off)")
+
 // ---------------------------------------------------------------------------------------------
 // math helpers (precision-overloaded).
 // f64 (parity builds) uses the OCML functions.  f32 (the benchmark precision) uses the CDNA4
@@ -177,6 +184,7 @@ __device__ __forceinline__ T h_circle_k(int i, T px, T py) {  // :16-30
 #endif
 template <typename T>
 __device__ __forceinline__ const DSpec<T>& obs_tab(const DSpec<T>& s) {
+  DTMPC_NOCONTRACT
 #ifdef DTMPC_OBS_REGS
   return s;
 #else
@@ -200,6 +208,7 @@ __device__ __forceinline__ T h_circle(const DSpec<T>& s, int i, T px, T py) {  /
 // an ulp and a contracted fma(dx, dx, dy*dy) picks the other obstacle than the reference does.
 template <typename T>
 __device__ __forceinline__ T h_circle_exact(const DSpec<T>&, int i, T px, T py) {
+  DTMPC_NOCONTRACT
 #pragma clang fp contract(off)
   const DSpec<T>& k = kspec<T>();
   T dx = px - k.cx[i];
@@ -218,6 +227,7 @@ constexpr int kFastObs = 8;
 
 template <typename T, int MO>
 __device__ __forceinline__ T h_smoothmin1(const DSpec<T>& s, T px, T py) {
+  DTMPC_NOCONTRACT
   T hm = h_circle(s, 0, px, py);
 #pragma unroll
   for (int i = 1; i < MO; ++i) hm = m_min(hm, h_circle(s, i, px, py));
@@ -233,6 +243,7 @@ __device__ __forceinline__ T h_smoothmin1(const DSpec<T>& s, T px, T py) {
 // tube step 8.14 -> 7.48 ms at B = 65,536 (round 1, v6).
 template <typename T, int W, int MO>
 __device__ __forceinline__ void h_smoothmin_w(const DSpec<T>& s, const T* px, const T* py, T* h) {
+  DTMPC_NOCONTRACT
   T hi[MO][W], hm[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) hm[w] = hi[0][w] = h_circle(s, 0, px[w], py[w]);
@@ -255,6 +266,7 @@ __device__ __forceinline__ void h_smoothmin_w(const DSpec<T>& s, const T* px, co
 
 template <typename T, int W>
 __device__ __forceinline__ void h_vec(const DSpec<T>& s, const T* px, const T* py, T* h) {
+  DTMPC_NOCONTRACT
 #ifndef DTMPC_LS_RUNTIME_OBS
   if constexpr (W > 1) {
     if (s.agg == DTMPC_OBS_SMOOTHMIN && s.M > 0 && s.M <= kFastObs) {
@@ -417,6 +429,7 @@ __device__ __forceinline__ T h_grad(const DSpec<T>& s, T px, T py, T& gx, T& gy)
 // relaxed_inverse_barrier_B_alpha core/barrier.py:36-59, alpha_eff = max(alpha, eps)
 template <typename T>
 __device__ __forceinline__ T barrier_relaxed(const DSpec<T>& s, T z) {
+  DTMPC_NOCONTRACT
   T a = s.alpha > s.eps ? s.alpha : s.eps;
   if (z >= a) {
     T zc = z < s.eps ? s.eps : z;
@@ -443,6 +456,7 @@ __device__ __forceinline__ T dbarrier_relaxed(const DSpec<T>& s, T z) {
 // barrier inside the DBaS dynamics (core/barrier.py:99-106; log: barrier_B :62-72)
 template <typename T>
 __device__ __forceinline__ T barrier_dyn(const DSpec<T>& s, T z) {
+  DTMPC_NOCONTRACT
   if (s.barrier == DTMPC_BARRIER_LOG) {
     T zc = z < s.eps ? s.eps : z;
     return -m_log(zc);
@@ -460,6 +474,7 @@ __device__ __forceinline__ T barrier_dyn(const DSpec<T>& s, T z) {
 template <typename T, int W>
 __device__ __forceinline__ void fhat_vec(const DSpec<T>& s, T* x0, T* x1, T* x2, T* b,
                                          const T* u0, const T* u1, T* Bc) {
+  DTMPC_NOCONTRACT
   T hn[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) {
@@ -481,6 +496,7 @@ __device__ __forceinline__ void fhat_vec(const DSpec<T>& s, T* x0, T* x1, T* x2,
 
 template <typename T>
 __device__ __forceinline__ T barrier_of_state(const DSpec<T>& s, T px, T py) {
+  DTMPC_NOCONTRACT
   T h[1], x[1] = {px}, y[1] = {py};
   h_vec<T, 1>(s, x, y, h);
   return barrier_dyn(s, h[0] - s.tight);
@@ -492,6 +508,7 @@ __device__ __forceinline__ T barrier_of_state(const DSpec<T>& s, T px, T py) {
 template <typename T>
 __device__ __forceinline__ T stage_cost(const DCost<T>& c, T x0, T x1, T x2, T b, T u0, T u1,
                                         T r0, T r1, T r2, T ur0, T ur1) {
+  DTMPC_NOCONTRACT
   T d0, d1, d2, e0, e1;
   if (c.kind == DTMPC_COST_TRACK) {
     d0 = x0 - r0;
@@ -514,6 +531,7 @@ __device__ __forceinline__ T stage_cost(const DCost<T>& c, T x0, T x1, T x2, T b
 
 template <typename T>
 __device__ __forceinline__ T term_cost(const DCost<T>& c, T x0, T x1, T x2, T b, T r0, T r1, T r2) {
+  DTMPC_NOCONTRACT
   T d0, d1, d2;
   if (c.kind == DTMPC_COST_TRACK) {
     d0 = x0 - r0;

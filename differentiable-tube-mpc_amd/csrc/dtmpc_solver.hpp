@@ -268,6 +268,7 @@ __device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c,
                                            const T* x0, T Bc0, const Col<T>& X, const Col<T>& U,
                                            const G& gains, const Col<T>& Xr, int rf,
                                            const Col<T>& Ur, T Jprev, T& bestJ, T& al_out) {
+  DTMPC_NOCONTRACT
   const int N = s.N;
   T a0[NC], a1[NC], a2[NC], ab[NC], Bc[NC], J[NC];
 #pragma unroll
@@ -366,6 +367,7 @@ __device__ __forceinline__ int line_search_pair(const DSpec<T>& s, const DCost<T
                                                 const T* x0, T Bc0, const Col<T>& X, const Col<T>& U,
                                                 const G& gains, const Col<T>& Xr, int rf,
                                                 const Col<T>& Ur, T Jprev, T& bestJ, T& al_out, int h) {
+  DTMPC_NOCONTRACT
   constexpr int NL = (NC + 1) / 2;
   const int N = s.N;
   T a0[NL], a1[NL], a2[NL], ab[NL], Bc[NL], J[NL], al[NL];
@@ -477,6 +479,7 @@ __device__ __forceinline__ int line_search_pair(const DSpec<T>& s, const DCost<T
 template <typename T>
 __device__ __forceinline__ T tape_cost(const DCost<T>& c, const Col<T>& X, const Col<T>& U,
                                        const Col<T>& Xr, int rf, const Col<T>& Ur, int N) {
+  DTMPC_NOCONTRACT
   T J = T(0);
   for (int k = 0; k < N; ++k) {
     T r0, r1, r2, q0, q1;
@@ -496,6 +499,7 @@ __device__ __forceinline__ T tape_cost(const DCost<T>& c, const Col<T>& X, const
 template <typename T, typename G>
 __device__ __forceinline__ void commit_candidate(const DSpec<T>& s, T al, const T* x0, T Bc0, const Col<T>& X,
                                  const Col<T>& U, const G& gains) {
+  DTMPC_NOCONTRACT
   const int N = s.N;
   T s0[1] = {x0[0]}, s1[1] = {x0[1]}, s2[1] = {x0[2]}, sb[1] = {x0[3]}, Bc[1] = {Bc0};
   DCost<T> none;
@@ -532,6 +536,7 @@ __device__ __forceinline__ void commit_candidate(const DSpec<T>& s, T al, const 
 // rollout core/ddp.py:89-99 (U used as stored)
 template <typename T>
 __device__ __forceinline__ void rollout_traj(const DSpec<T>& s, const T* x0, const Col<T>& X, const Col<T>& U) {
+  DTMPC_NOCONTRACT
   const int N = s.N;
   T s0[1] = {x0[0]}, s1[1] = {x0[1]}, s2[1] = {x0[2]}, sb[1] = {x0[3]};
   T Bc[1] = {barrier_of_state(s, x0[0], x0[1])};
@@ -548,6 +553,16 @@ __device__ __forceinline__ void rollout_traj(const DSpec<T>& s, const T* x0, con
     X.at(k + 1, 4, 3) = sb[0];
   }
 }
+
+}  // namespace dtmpc
+#include "dtmpc_ls_pk.hpp"
+namespace dtmpc {
+
+// f32, even candidate count: the line search on candidate pairs (packed-f32 VALU, dtmpc_ls_pk.hpp)
+#ifndef DTMPC_LS_PACKED
+#define DTMPC_LS_PACKED 1
+#endif
+constexpr bool kPackedLS = DTMPC_LS_PACKED != 0;
 
 // ---------------------------------------------------------------------------------------------
 // iLQR for one trajectory (core/ddp.py:102-307).  U: in V_init, out V*.  X: out X*.
@@ -583,6 +598,8 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
     int best;
     if constexpr (LPT == 2)
       best = line_search_pair<T, NA>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, Jcur, bestJ, al, h);
+    else if constexpr (kPackedLS && sizeof(T) == 4 && NA % 2 == 0)
+      best = line_search_pk<NA>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, Jcur, bestJ, al);
     else
       best = line_search<T, NA>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, Jcur, bestJ, al);
 #ifdef DTMPC_DIAG_LS2  // timing attribution only: the pass again (same decision)
