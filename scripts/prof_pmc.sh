@@ -4,7 +4,7 @@
 set -u
 TAG=${1:-r01}
 shift || true
-ARGS=${*:-"--steps 2 --warmup 1 --no-cpu"}
+ARGS=${*:-"--steps 8 --warmup 2 --no-cpu"}
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
