@@ -33,6 +33,37 @@ __device__ __forceinline__ pf2 pk_log(pf2 x) {  // m_log per element, the scalin
   return y * 0.693147180559945309f;
 }
 
+// m_sincos (dtmpc_device.hpp) on a pair: sincos_cw with every fma / mul packed; the rare element
+// outside |x| <= 65536 (or non-finite) sends the pair through the scalar function
+__device__ __forceinline__ void pk_sincos(pf2 x, pf2& sn, pf2& cs) {
+#ifndef DTMPC_OCML_SINCOS
+  if (__builtin_expect(__builtin_fabsf(x.x) <= 65536.0f && __builtin_fabsf(x.y) <= 65536.0f, 1)) {
+    const pf2 q = pf2{__builtin_rintf(x.x * k2oPi), __builtin_rintf(x.y * k2oPi)};
+    pf2 r = __builtin_elementwise_fma(-q, pf2(kPio2A), x);
+    r = __builtin_elementwise_fma(-q, pf2(kPio2B), r);
+    r = __builtin_elementwise_fma(-q, pf2(kPio2C), r);
+    const pf2 z = r * r;
+    pf2 ps = __builtin_elementwise_fma(z, pf2(kSinS3), pf2(kSinS2));
+    ps = __builtin_elementwise_fma(z, ps, pf2(kSinS1));
+    const pf2 s = __builtin_elementwise_fma(r * z, ps, r);
+    pf2 pc = __builtin_elementwise_fma(z, pf2(kCosK3), pf2(kCosK2));
+    pc = __builtin_elementwise_fma(z, pc, pf2(kCosK1));
+    const pf2 c = __builtin_elementwise_fma(z * z, pc, __builtin_elementwise_fma(pf2(-0.5f), z, pf2(1.0f)));
+    const int j0 = (int)q.x & 3, j1 = (int)q.y & 3;
+    const float so0 = (j0 & 1) ? c.x : s.x, co0 = (j0 & 1) ? s.x : c.x;
+    const float so1 = (j1 & 1) ? c.y : s.y, co1 = (j1 & 1) ? s.y : c.y;
+    sn = pf2{(j0 & 2) ? -so0 : so0, (j1 & 2) ? -so1 : so1};
+    cs = pf2{((j0 + 1) & 2) ? -co0 : co0, ((j1 + 1) & 2) ? -co1 : co1};
+    return;
+  }
+#endif
+  float s0, c0, s1, c1;
+  m_sincos(x.x, &s0, &c0);
+  m_sincos(x.y, &s1, &c1);
+  sn = pf2{s0, s1};
+  cs = pf2{c0, c1};
+}
+
 // stage_cost / term_cost of dtmpc_device.hpp on two candidates (TRACK, or TARGET without wrap; the
 // wrapped target goes element by element through the scalar function)
 __device__ __forceinline__ pf2 pk_stage_cost(const DCost<float>& c, pf2 x0, pf2 x1, pf2 x2, pf2 b, pf2 u0, pf2 u1,
@@ -113,10 +144,8 @@ __device__ __forceinline__ void pk_fhat(const DSpec<float>& s, pf2* x0, pf2* x1,
   PK_CONTRACT
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    float s0, c0, s1, c1;
-    m_sincos(x2[p].x, &s0, &c0);
-    m_sincos(x2[p].y, &s1, &c1);
-    const pf2 sn = pf2{s0, s1}, cs = pf2{c0, c1};
+    pf2 sn, cs;
+    pk_sincos(x2[p], sn, cs);
     pf2 dv = s.dt * u0[p];
     x0[p] = x0[p] + dv * cs;
     x1[p] = x1[p] + dv * sn;
