@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/dtmpc.h"
@@ -197,20 +198,25 @@ struct TubeArgs {
 };
 
 
-// kTubeLPT lanes per trajectory (1 or 2).  At the benchmark batch (65,536 trajectories) one lane per
-// trajectory is exactly one wave per SIMD and nothing hides latency; with 2 (paired line search,
-// line_search_pair) there are two waves per SIMD, each rolling out half the line-search candidates,
-// the rest of the step computed identically by both lanes of a pair (identical values stored twice).
-// Measured at B = 65,536: 2 lanes 8.27 ms vs 1 lane 7.54 ms (the 256-register cap of two waves per
-// SIMD spills 46 VGPRs to scratch, and the duplicated backward / commit work outweighs the overlap),
-// so the default is 1; the paired path stays parity-tested as a build option.
-#ifndef DTMPC_TUBE_LPT
-#define DTMPC_TUBE_LPT 1
-#endif
-constexpr int kTubeLPT = DTMPC_TUBE_LPT;
+// LPT lanes per trajectory (1 or 2), chosen per launch (tube_lanes).  At the benchmark batch (65,536
+// trajectories) one lane per trajectory is exactly one wave per SIMD; two lanes (paired line search,
+// line_search_pair: each lane of a pair rolls out half the candidates, the rest of the step is
+// computed identically by both lanes and stored twice) measured 8.27 vs 7.54 ms there -- the
+// duplicated backward / commit work outweighs the overlap.  Below kPairBatch trajectories the machine
+// is mostly idle and the step is ONE wave's latency, which the paired line search cuts: there the
+// tube step uses two lanes.  DTMPC_TUBE_LANES=1|2 (environment) forces either, for the parity tests.
+constexpr int64_t kPairBatch = 16384;  // <= 512 paired waves: at most half a wave per SIMD
 
-template <typename T, int NA>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kTubeLPT, kTubeLPT)))
+static int tube_lanes(int64_t B) {
+  const char* e = getenv("DTMPC_TUBE_LANES");
+  if (e && (e[0] == '1' || e[0] == '2') && e[1] == 0) return e[0] - '0';
+  return B <= kPairBatch ? 2 : 1;
+}
+
+// One wave per SIMD is all either form gets (the two-lane form runs only at small batches), so the
+// full 512-register budget, no spill.
+template <typename T, int NA, int LPT>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeArgs<T> a) {
   __shared__ T red[kBlock / 64][8];
   DSpec<T> s = s_arg;
@@ -220,7 +226,7 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
   const int B = a.B;
   const int N = s.N;
   const int gl = blockIdx.x * kBlock + threadIdx.x;
-  const int i = gl / kTubeLPT, hl = gl % kTubeLPT;
+  const int i = gl / LPT, hl = gl % LPT;
   T acc[7] = {T(0), T(0), T(0), T(0), T(0), T(0), T(0)};
   if (i < B) {
     const size_t nb = (size_t)B;
@@ -241,7 +247,7 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
     // SoA cells of other lanes, which other waves may be writing in their sensitivity pass meanwhile.
     const GainsAoS<T> gains{a.work + (size_t)N * 20 * nb, a.work + (size_t)N * 28 * nb, (unsigned)B,
                             (unsigned)i};
-    st |= ilqr_traj<T, NA, kTubeLPT>(s, cn, cfn, xn0, Xn, Un, gains, none, 0, none, itn, pr, 0, hl);
+    st |= ilqr_traj<T, NA, LPT>(s, cn, cfn, xn0, Xn, Un, gains, none, 0, none, itn, pr, 0, hl);
     // ancillary MPC tracking the nominal plan :863-909 (terminal weight Qa, :885, :891)
     DCost<T> ca;
     ca.kind = DTMPC_COST_TRACK;
@@ -255,7 +261,7 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
     ca.t0 = ca.t1 = ca.t2 = T(0);
     T xa0[4] = {x0, x1, x2, xb};
     pr.mark(8);
-    st |= ilqr_traj<T, NA, kTubeLPT>(s, ca, cfa, xa0, Xa, Ua, gains, Xn, 4, Un, ita, pr, 4, hl);
+    st |= ilqr_traj<T, NA, LPT>(s, ca, cfa, xa0, Xa, Ua, gains, Xn, 4, Un, ita, pr, 4, hl);
     pr.mark(8);
     // upper loss, DOC sensitivity and analytic gradient :915-976
     st |= sens_traj<T, false, false, true>(s, ca, Xa, Ua, Xn, 4, Un, Xn, 4, K, kf, AB, none, none,
@@ -448,10 +454,14 @@ static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B
     a.whi[f] = T(cf->w_high[f]);
   }
   // the fused kernel runs both solves with one line-search width (same alphas, checked)
+  const int lpt = tube_lanes(B);
   switch (cfn.nc) {
 #define CASE(n)                                                                                     \
   case n:                                                                                           \
-    hipLaunchKernelGGL((tube_step_kernel<T, n>), grid_for(B * kTubeLPT), dim3(kBlock), 0, st, s, cn, cfn, cfa, a); \
+    if (lpt == 2)                                                                                   \
+      hipLaunchKernelGGL((tube_step_kernel<T, n, 2>), grid_for(B * 2), dim3(kBlock), 0, st, s, cn, cfn, cfa, a); \
+    else                                                                                            \
+      hipLaunchKernelGGL((tube_step_kernel<T, n, 1>), grid_for(B), dim3(kBlock), 0, st, s, cn, cfn, cfa, a); \
     break;
     DTMPC_NA_CASES(CASE)
 #undef CASE
@@ -610,7 +620,7 @@ size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
   return el * (size_t)horizon * 30 * (size_t)B;  // sensitivity K / kf / AB (SoA, 20) + iLQR gains (AoS, 10)
 }
 
-int64_t dtmpc_tube_partials_count(int64_t B) { return (B * kTubeLPT + kBlock - 1) / kBlock; }
+int64_t dtmpc_tube_partials_count(int64_t B) { return (B * tube_lanes(B) + kBlock - 1) / kBlock; }
 
 int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B,
                     int64_t global_offset, int64_t step, const dtmpc_tube_state* state,

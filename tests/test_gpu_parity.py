@@ -333,15 +333,20 @@ def _oracle_tube(o, st, x0b, steps, B, seed):
     return xs, ths, sts
 
 
+@pytest.mark.parametrize("lanes", ["auto", "1"])
 @pytest.mark.parametrize("mode", ["paper", "bench"])
 @pytest.mark.parametrize("tag", ["f64", "f32"])
-def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode):
+def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode, lanes, monkeypatch):
     """Fused Algorithm-2 step (device Philox disturbances) on the bench workload's start distribution
     (x0 ~ U[0,1]^2 x U[0, pi/2], zero warm starts), ragged batch, 3 closed-loop steps: per-trajectory
     plant / nominal states, warm starts and the shared theta, against the three oracle builds.
+    lanes: the step's kernel at this batch size runs two lanes per trajectory (paired line search,
+    "auto"); "1" forces the one-lane kernel of the large batches (DTMPC_TUBE_LANES).
     mode paper: tol = 1e-3 early exit (core/tube_mpc.py:757-768); bench: fixed iterations (tol = -1).
     In f32 the paper's absolute tol test sits at fp32 resolution of the cost, so
     iteration counts flip on a few % of trajectories there; the bench mode has no such decision."""
+    if lanes != "auto":
+        monkeypatch.setenv("DTMPC_TUBE_LANES", lanes)
     import dataclasses
 
     from diff_tube_mpc_strict_pt.core import TubeMPC
