@@ -776,6 +776,18 @@ __device__ __forceinline__ bool riccati_step(const Jac<T>& J, const T* lx, const
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) M2[i][j] = K[i] * Qux[0][j] + K[4 + i] * Qux[1][j];
+#ifdef DTMPC_VXX_SYM
+  // V_xx is symmetric in exact arithmetic: the upper triangle is computed and mirrored (the reference's
+  // full product differs from its transpose by rounding only); the lower half of Q_xx then goes dead.
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = i; j < 4; ++j) {
+      T m1 = KQ[i][0] * K[j] + KQ[i][1] * K[4 + j];
+      R.Vxx[i][j] = Qxx[i][j] + m1 + M2[i][j] + M2[j][i];
+      R.Vxx[j][i] = R.Vxx[i][j];
+    }
+#else
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -783,6 +795,7 @@ __device__ __forceinline__ bool riccati_step(const Jac<T>& J, const T* lx, const
       T m1 = KQ[i][0] * K[j] + KQ[i][1] * K[4 + j];
       R.Vxx[i][j] = Qxx[i][j] + m1 + M2[i][j] + M2[j][i];
     }
+#endif
   return ok;
 }
 
