@@ -493,6 +493,50 @@ __device__ __forceinline__ T tape_cost(const DCost<T>& c, const Col<T>& X, const
   return J + term_cost(c, T(X.at(N, 4, 0)), T(X.at(N, 4, 1)), T(X.at(N, 4, 2)), T(X.at(N, 4, 3)), r0, r1, r2);
 }
 
+// iLQR start (core/ddp.py:127-131 + the alpha = 0 candidate's cost): V = clamp(V_init), X = rollout(x0, V)
+// and, if want_cost, the tape's cost -- one pass with U (and the references) prefetched one step ahead,
+// instead of a clamp pass, a dependent-load rollout pass and a tape_cost pass.  Same operations in the
+// same order as clamp + rollout_traj + tape_cost.
+template <typename T>
+__device__ __forceinline__ T init_tape(const DSpec<T>& s, const DCost<T>& c, const T* x0, const Col<T>& X,
+                                       const Col<T>& U, const Col<T>& Xr, int rf, const Col<T>& Ur,
+                                       bool want_cost) {
+  DTMPC_NOCONTRACT
+  const int N = s.N;
+  T s0[1] = {x0[0]}, s1[1] = {x0[1]}, s2[1] = {x0[2]}, sb[1] = {x0[3]};
+  T Bc[1] = {barrier_of_state(s, x0[0], x0[1])};
+  X.at(0, 4, 0) = s0[0];
+  X.at(0, 4, 1) = s1[0];
+  X.at(0, 4, 2) = s2[0];
+  X.at(0, 4, 3) = sb[0];
+  T J = T(0);
+  T n0 = U.at(0, 2, 0), n1 = U.at(0, 2, 1), nr0, nr1, nr2, nq0, nq1;
+  load_ref(c, Xr, rf, 0, nr0, nr1, nr2);
+  load_uref(c, Ur, 0, nq0, nq1);
+  for (int k = 0; k < N; ++k) {
+    const T v0 = n0, v1 = n1, r0 = nr0, r1 = nr1, r2 = nr2, q0 = nq0, q1 = nq1;
+    if (k + 1 < N) {
+      n0 = U.at(k + 1, 2, 0);
+      n1 = U.at(k + 1, 2, 1);
+      load_ref(c, Xr, rf, k + 1, nr0, nr1, nr2);
+      load_uref(c, Ur, k + 1, nq0, nq1);
+    }
+    T u0[1] = {clampv(v0, s.umin0, s.umax0)}, u1[1] = {clampv(v1, s.umin1, s.umax1)};
+    U.at(k, 2, 0) = u0[0];
+    U.at(k, 2, 1) = u1[0];
+    if (want_cost) J = J + stage_cost(c, s0[0], s1[0], s2[0], sb[0], u0[0], u1[0], r0, r1, r2, q0, q1);
+    fhat_vec<T, 1>(s, s0, s1, s2, sb, u0, u1, Bc);
+    X.at(k + 1, 4, 0) = s0[0];
+    X.at(k + 1, 4, 1) = s1[0];
+    X.at(k + 1, 4, 2) = s2[0];
+    X.at(k + 1, 4, 3) = sb[0];
+  }
+  if (!want_cost) return T(0);
+  T r0, r1, r2;
+  load_ref(c, Xr, rf, N, r0, r1, r2);
+  return J + term_cost(c, s0[0], s1[0], s2[0], sb[0], r0, r1, r2);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Materialise the chosen candidate in place: X, U <- rollout with step alpha (same arithmetic
 // as the candidate lane of line_search).  X[k+1] of the old tape is read before it is replaced.
@@ -573,15 +617,10 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
                          const Col<T>& Xr, int rf, const Col<T>& Ur, int& iters, Prof& pr,
                          int pb, int h = 0) {
   const int N = s.N;
-  // V = clamp(V_init); X = rollout(x0, V)   (:127-131)
-  for (int k = 0; k < N; ++k) {
-    U.at(k, 2, 0) = clampv(T(U.at(k, 2, 0)), s.umin0, s.umax0);
-    U.at(k, 2, 1) = clampv(T(U.at(k, 2, 1)), s.umin1, s.umax1);
-  }
-  rollout_traj(s, x0, X, U);
+  // V = clamp(V_init); X = rollout(x0, V)   (:127-131); the cost of that tape is the alpha = 0
+  // candidate's cost (only needed when alpha = 0 is listed)
+  T Jcur = init_tape(s, c, x0, X, U, Xr, rf, Ur, cfg.zpos >= 0 && cfg.max_iter > 0);
   T Bc0 = barrier_of_state(s, x0[0], x0[1]);
-  // cost of the current tape = the alpha = 0 candidate's cost (only needed when alpha = 0 is listed)
-  T Jcur = cfg.zpos >= 0 && cfg.max_iter > 0 ? tape_cost(c, X, U, Xr, rf, Ur, N) : T(0);
   pr.mark(pb + 0);
   bool have_prev = false;
   T prev = T(0);
