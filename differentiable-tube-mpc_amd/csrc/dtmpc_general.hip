@@ -118,8 +118,8 @@ struct GenArgs {
   T* Uaux;
   T* work;
   const T* theta;  // [2][12] raw
-  T* partials;     // [nblocks][24]
-  T* gout;         // [24][B] or null
+  T* partials;     // [nblocks][DTMPC_GEN_SUMS]
+  T* gout;         // [25][B] or null
   int* status;
   int* iters;
 };
@@ -176,14 +176,19 @@ __global__ void __launch_bounds__(kBlock) general_step_kernel(DSpec<T> s, DIlqr<
 #pragma unroll
       for (int j = 0; j < 12; ++j) acc[12 + j] = g[j];
     }
+    // healthy-trajectory count (slot 24).  A flagged trajectory contributes nothing to the batch
+    // sums -- neither L nor gradients nor the count -- so the update's mean runs over the healthy
+    // ones (the paper step does the same); its gout keeps L (row 0, logged by the plant) and zero
+    // gradients.
+    acc[DTMPC_GEN_SUMS - 1] = st ? T(0) : T(1);
     if (a.gout) {
+      a.gout[i] = acc[0];
 #pragma unroll
-      for (int j = 0; j < DTMPC_GEN_SUMS; ++j) a.gout[(size_t)j * nb + i] = st ? T(0) : acc[j];
+      for (int j = 1; j < DTMPC_GEN_SUMS; ++j) a.gout[(size_t)j * nb + i] = st ? T(0) : acc[j];
     }
-    // a flagged trajectory contributes nothing to the shared gradient; its L is kept for the log
     if (st) {
 #pragma unroll
-      for (int j = 1; j < DTMPC_GEN_SUMS; ++j) acc[j] = T(0);
+      for (int j = 0; j < DTMPC_GEN_SUMS; ++j) acc[j] = T(0);
     }
     a.status[i] |= st;
     if (a.iters) {
@@ -266,6 +271,11 @@ template <typename T>
 __global__ void general_update_kernel(T lr, T mom, double clip, int project, int adapt_anc, int adapt_nom,
                                       int alpha_used, T ib, const T* sums, T* theta, T* vel) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  // ib <= 0: mean over the healthy trajectories counted in the last slot
+  if (!(ib > T(0))) {
+    const T cnt = sums[DTMPC_GEN_SUMS - 1];
+    ib = cnt > T(0) ? T(1) / cnt : T(0);
+  }
   for (int set = 0; set < 2; ++set) {
     if (set == 0 && !adapt_anc) continue;
     if (set == 1 && !adapt_nom) continue;
@@ -526,6 +536,8 @@ int dtmpc_ift_gradient(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost
   return check_launch("ift_kernel");
 }
 
+int64_t dtmpc_general_partials_count(int64_t B) { return B < 1 ? 0 : (B + kBlock - 1) / kBlock; }
+
 size_t dtmpc_general_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
   size_t el = dtype == DTMPC_F64 ? 8 : 4;
   return el * ((size_t)horizon * 20 + (size_t)(horizon + 1) * 10) * (size_t)B;
@@ -538,6 +550,8 @@ int dtmpc_general_step(int dtype, const dtmpc_spec* spec, const dtmpc_general_cf
   const dtmpc_general_state* S = state;
   if (!S->Xnom || !S->Xaux || !S->work || !S->partials || !S->status)
     return set_err(DTMPC_ERR_BAD_ARG, "NULL state array");
+  if (S->n_partials < dtmpc_general_partials_count(B))
+    return set_err(DTMPC_ERR_BAD_ARG, "state->n_partials < dtmpc_general_partials_count(B)");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DTMPC_F32) return launch_general<float>(spec, cfg, B, S, st);
   if (dtype == DTMPC_F64) return launch_general<double>(spec, cfg, B, S, st);

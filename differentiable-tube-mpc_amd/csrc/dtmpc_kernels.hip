@@ -204,10 +204,11 @@ struct TubeArgs {
 // computed identically by both lanes and stored twice) measured 8.27 vs 7.54 ms there -- the
 // duplicated backward / commit work outweighs the overlap.  Below kPairBatch trajectories the machine
 // is mostly idle and the step is ONE wave's latency, which the paired line search cuts: there the
-// tube step uses two lanes.  DTMPC_TUBE_LANES=1|2 (environment) forces either, for the parity tests.
+// tube step uses two lanes.  DTMPC_TUBE_LANES=1|2 (environment) forces either, for the parity tests;
+// it is read by dtmpc_tube_lanes only, i.e. once, when the caller builds its state (state->lanes).
 constexpr int64_t kPairBatch = 16384;  // <= 512 paired waves: at most half a wave per SIMD
 
-static int tube_lanes(int64_t B) {
+static int tube_lanes_default(int64_t B) {
   const char* e = getenv("DTMPC_TUBE_LANES");
   if (e && (e[0] == '1' || e[0] == '2') && e[1] == 0) return e[0] - '0';
   return B <= kPairBatch ? 2 : 1;
@@ -218,7 +219,7 @@ static int tube_lanes(int64_t B) {
 template <typename T, int NA, int LPT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeArgs<T> a) {
-  __shared__ T red[kBlock / 64][8];
+  __shared__ T red[kBlock / 64][DTMPC_TUBE_SUMS];
   DSpec<T> s = s_arg;
 #ifdef DTMPC_OBS_REGS
   obs_pin(s);  // obstacle table in VGPRs for the whole step (obs_tab)
@@ -227,7 +228,7 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
   const int N = s.N;
   const int gl = blockIdx.x * kBlock + threadIdx.x;
   const int i = gl / LPT, hl = gl % LPT;
-  T acc[7] = {T(0), T(0), T(0), T(0), T(0), T(0), T(0)};
+  T acc[DTMPC_TUBE_SUMS] = {T(0), T(0), T(0), T(0), T(0), T(0), T(0), T(0)};
   if (i < B) {
     const size_t nb = (size_t)B;
     Col<T> Xn = col<T>(a.Xnom, i, B), Un = col<T>(a.Unom, i, B), Xa = col<T>(a.Xaux, i, B),
@@ -325,9 +326,12 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
       Ua.at(k, 2, 0) = Ua.at(k + 1, 2, 0);
       Ua.at(k, 2, 1) = Ua.at(k + 1, 2, 1);
     }
-    if (st || hl != 0) {  // a failed trajectory contributes nothing; a pair counts once
+    // batch sums over the healthy trajectories only (L and gradients, and their count in slot 7):
+    // a flagged trajectory drops out of the mean; a pair counts once
+    acc[7] = T(1);
+    if (st || hl != 0) {
 #pragma unroll
-      for (int j = 0; j < 7; ++j) acc[j] = T(0);
+      for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) acc[j] = T(0);
     }
     a.status[i] |= st;
     if (a.iters) {
@@ -337,21 +341,19 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
     pr.mark(10);
     pr.flush();
   }
-  // fixed-order workgroup sum of [L, gQ, gR, gqb]
+  // fixed-order workgroup sum of [L, gQ, gR, gqb, count]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-  for (int j = 0; j < 7; ++j) {
+  for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) {
     T v = wave_sum(acc[j]);
     if (lane == 0) red[wv][j] = v;
   }
   __syncthreads();
-  if (threadIdx.x < 8) {
+  if (threadIdx.x < DTMPC_TUBE_SUMS) {
     T v = T(0);
-    if (threadIdx.x < 7) {
 #pragma unroll
-      for (int q = 0; q < kBlock / 64; ++q) v += red[q][threadIdx.x];
-    }
-    a.partials[(size_t)blockIdx.x * 8 + threadIdx.x] = v;
+    for (int q = 0; q < kBlock / 64; ++q) v += red[q][threadIdx.x];
+    a.partials[(size_t)blockIdx.x * DTMPC_TUBE_SUMS + threadIdx.x] = v;
   }
 }
 
@@ -374,11 +376,13 @@ __global__ void __launch_bounds__(kBlock) partials_reduce_kernel(int64_t n, cons
   if (threadIdx.x < 8) sums[threadIdx.x] = red[0][threadIdx.x];
 }
 
-// momentum + projected update (core/tube_mpc.py:978-984)
+// momentum + projected update (core/tube_mpc.py:978-984); inv_batch <= 0: mean over the healthy
+// trajectories counted in sums[7]
 template <typename T>
 __global__ void theta_update_kernel(T mom, T eta, T qmin, T rmin, T qbmin, T qbmax, T inv_batch,
                                     const T* sums, T* theta, T* vel) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (!(inv_batch > T(0))) inv_batch = sums[7] > T(0) ? T(1) / sums[7] : T(0);
   for (int j = 0; j < 6; ++j) {
     T g = sums[1 + j] * inv_batch;
     vel[j] = mom * vel[j] + g;
@@ -423,6 +427,7 @@ static int launch_ilqr(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_i
 template <typename T>
 static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff,
                        int64_t step, const dtmpc_tube_state* S, const void* w, hipStream_t st) {
+  const int lpt = S->lanes;
   DSpec<T> s = make_spec<T>(*sp);
   DCost<T> cn = make_cost<T>(cf->nominal);
   DIlqr<T> cfn = make_ilqr<T>(cf->nom_ilqr), cfa = make_ilqr<T>(cf->aux_ilqr);
@@ -454,7 +459,6 @@ static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B
     a.whi[f] = T(cf->w_high[f]);
   }
   // the fused kernel runs both solves with one line-search width (same alphas, checked)
-  const int lpt = tube_lanes(B);
   switch (cfn.nc) {
 #define CASE(n)                                                                                     \
   case n:                                                                                           \
@@ -620,7 +624,12 @@ size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
   return el * (size_t)horizon * 30 * (size_t)B;  // sensitivity K / kf / AB (SoA, 20) + iLQR gains (AoS, 10)
 }
 
-int64_t dtmpc_tube_partials_count(int64_t B) { return (B * tube_lanes(B) + kBlock - 1) / kBlock; }
+int32_t dtmpc_tube_lanes(int64_t B) { return tube_lanes_default(B); }
+
+int64_t dtmpc_tube_partials_count(int64_t B, int32_t lanes) {
+  if (B < 1 || (lanes != 1 && lanes != 2)) return 0;
+  return (B * lanes + kBlock - 1) / kBlock;
+}
 
 int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B,
                     int64_t global_offset, int64_t step, const dtmpc_tube_state* state,
@@ -639,6 +648,9 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
   if (!S->x || !S->b || !S->xbar || !S->bbar || !S->Xnom || !S->Unom || !S->Xaux || !S->Uaux ||
       !S->work || !S->theta || !S->partials || !S->status)
     return set_err(DTMPC_ERR_BAD_ARG, "NULL state array");
+  if (S->lanes != 1 && S->lanes != 2) return set_err(DTMPC_ERR_BAD_ARG, "state->lanes must be 1 or 2");
+  if (S->n_partials < dtmpc_tube_partials_count(B, S->lanes))
+    return set_err(DTMPC_ERR_BAD_ARG, "state->n_partials < dtmpc_tube_partials_count(B, lanes)");
   if (cfg->disturbance == 0 && !w) return set_err(DTMPC_ERR_BAD_ARG, "injected disturbance w is NULL");
   if (cfg->disturbance != 0 && cfg->disturbance != 1) return set_err(DTMPC_ERR_BAD_ARG, "bad disturbance mode");
   hipStream_t st = (hipStream_t)stream;

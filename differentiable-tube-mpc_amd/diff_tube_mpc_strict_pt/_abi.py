@@ -7,13 +7,14 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_OBS = 16
 MAX_ALPHAS = 8
 MAX_HORIZON = 512
 LOG_FIELDS = 18
 GEN_LOG_FIELDS = 12
-GEN_SUMS = 24
+GEN_SUMS = 25  # L, ancillary grads (11), nominal grads (12), healthy count
+TUBE_SUMS = 8  # L, gQ(3), gR(2), gqb, healthy count
 # raw parameter layout of the general path (include/dtmpc.h DTMPC_P_*)
 P_Q, P_R, P_QF, P_QB, P_ALPHA, P_GAMMA, P_TIGHT, P_COUNT = 0, 3, 5, 8, 9, 10, 11, 12
 
@@ -111,6 +112,9 @@ class DtmpcTubeState(C.Structure):
         ("log", C.c_void_p),
         ("status", C.c_void_p),
         ("iters", C.c_void_p),
+        ("lanes", C.c_int32),
+        ("pad_", C.c_int32),
+        ("n_partials", C.c_int64),
     ]
 
 
@@ -153,6 +157,7 @@ class DtmpcGeneralState(C.Structure):
         ("log", C.c_void_p),
         ("status", C.c_void_p),
         ("iters", C.c_void_p),
+        ("n_partials", C.c_int64),
     ]
 
 
@@ -179,7 +184,8 @@ PROTOTYPES = {
     ),
     "dtmpc_doc_grad": (C.c_int, [C.c_int, I32, I64, P, P, P, P, P, P, P, P]),
     "dtmpc_tube_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64]),
-    "dtmpc_tube_partials_count": (I64, [I64]),
+    "dtmpc_tube_lanes": (I32, [I64]),
+    "dtmpc_tube_partials_count": (I64, [I64, I32]),
     "dtmpc_tube_step": (
         C.c_int,
         [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcTubeCfg), I64, I64, I64, C.POINTER(DtmpcTubeState), P, P],
@@ -197,6 +203,7 @@ PROTOTYPES = {
          P, P],
     ),
     "dtmpc_general_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64]),
+    "dtmpc_general_partials_count": (I64, [I64]),
     "dtmpc_general_step": (
         C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcGeneralCfg), I64, C.POINTER(DtmpcGeneralState), P]),
     "dtmpc_partials_reduce_n": (C.c_int, [C.c_int, I64, I32, P, P, P]),

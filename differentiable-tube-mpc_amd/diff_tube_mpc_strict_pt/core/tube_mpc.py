@@ -62,11 +62,18 @@ def shard_range(global_batch: int, rank: int, world_size: int) -> Tuple[int, int
 
 
 def allreduce_sums(sums: Tensor, group=None) -> Tensor:
-    """Sum the [L, gQ(3), gR(2), gqb, 0] vector over ranks (RCCL on HIP devices, gloo on CPU)."""
+    """Sum the [L, gQ(3), gR(2), gqb, count] vector (or the general path's 25) over ranks (RCCL on HIP
+    devices, gloo on CPU)."""
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+        if sums.is_cuda and dist.get_backend(group) == "gloo":
+            # gloo (ranks sharing one device, where RCCL refuses): through host memory
+            host = sums.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            sums.copy_(host)
+        else:
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
     return sums
 
 
@@ -131,9 +138,11 @@ class TubeMPC:
         self.Uaux = torch.zeros(N, 2, B, **kw)
         self.work = torch.empty(self.lib.dtmpc_tube_workspace_bytes(self._dt, N, B), dtype=torch.uint8,
                                 device=self.device)
-        self.n_partials = int(self.lib.dtmpc_tube_partials_count(B))
-        self.partials = torch.zeros(self.n_partials, 8, **kw)
-        self.sums = torch.zeros(8, **kw)
+        # lanes per trajectory: resolved once here (DTMPC_TUBE_LANES is read by the library only now)
+        self.lanes = int(self.lib.dtmpc_tube_lanes(B))
+        self.n_partials = int(self.lib.dtmpc_tube_partials_count(B, self.lanes))
+        self.partials = torch.zeros(self.n_partials, _abi.TUBE_SUMS, **kw)
+        self.sums = torch.zeros(_abi.TUBE_SUMS, **kw)
         self._theta0 = torch.tensor(setup.theta0, **kw)
         self.theta = self._theta0.clone()
         self.vel = torch.zeros(6, **kw)
@@ -150,6 +159,8 @@ class TubeMPC:
         st.log = self.log.data_ptr() if self.log is not None else None
         st.status = self.status.data_ptr()
         st.iters = self.iters.data_ptr()
+        st.lanes = self.lanes
+        st.n_partials = self.n_partials
         self.state = st
 
     # -----------------------------------------------------------------------------------------
@@ -198,7 +209,8 @@ class TubeMPC:
         _lib.check(self.lib.dtmpc_partials_reduce(self._dt, self.n_partials, self.partials.data_ptr(),
                                                   self.sums.data_ptr(), s), "dtmpc_partials_reduce")
         allreduce_sums(self.sums, self.group)
-        _lib.check(self.lib.dtmpc_theta_update(self._dt, C.byref(self.adapt), 1.0 / self.global_batch,
+        # inv_batch 0: batch mean over the healthy trajectories (sums[7] counts them across ranks)
+        _lib.check(self.lib.dtmpc_theta_update(self._dt, C.byref(self.adapt), 0.0,
                                                self.sums.data_ptr(), self.theta.data_ptr(), self.vel.data_ptr(), s),
                    "dtmpc_theta_update")
         self.t += 1
@@ -209,7 +221,14 @@ class TubeMPC:
     # convenience views (trajectory-major copies)
     @property
     def loss_mean(self) -> float:
-        return float(self.sums[0]) / self.global_batch
+        """Mean upper loss of the last step over the healthy trajectories of the global batch."""
+        n = float(self.sums[_abi.TUBE_SUMS - 1])
+        return float(self.sums[0]) / n if n > 0 else float("nan")
+
+    @property
+    def healthy_count(self) -> int:
+        """Trajectories of the global batch that contributed to the last step's mean gradient."""
+        return int(round(float(self.sums[_abi.TUBE_SUMS - 1])))
 
     def nominal_tape(self):
         return self.Xnom.permute(2, 0, 1), self.Unom.permute(2, 0, 1)
@@ -258,7 +277,7 @@ class GeneralTubeMPC:
         self.Uaux = torch.zeros(N, 2, B, **kw)
         self.work = torch.empty(self.lib.dtmpc_general_workspace_bytes(self._dt, N, B), dtype=torch.uint8,
                                 device=self.device)
-        self.n_partials = int(self.lib.dtmpc_tube_partials_count(B))
+        self.n_partials = int(self.lib.dtmpc_general_partials_count(B))
         self.partials = torch.zeros(self.n_partials, _abi.GEN_SUMS, **kw)
         self.sums = torch.zeros(_abi.GEN_SUMS, **kw)
         self._theta0 = torch.tensor(setup.theta0, **kw)
@@ -281,6 +300,7 @@ class GeneralTubeMPC:
         st.log = self.log.data_ptr() if self.log is not None else None
         st.status = self.status.data_ptr()
         st.iters = self.iters.data_ptr()
+        st.n_partials = self.n_partials
         self.state = st
 
     def _stream(self) -> int:
@@ -339,8 +359,9 @@ class GeneralTubeMPC:
                                                     self.partials.data_ptr(), self.sums.data_ptr(), s),
                    "dtmpc_partials_reduce_n")
         allreduce_sums(self.sums, self.group)
+        # inv_batch 0: batch mean over the healthy trajectories (sums[24] counts them across ranks)
         _lib.check(self.lib.dtmpc_general_update(self._dt, C.byref(self.spec), C.byref(self.cfg),
-                                                 1.0 / self.global_batch, C.byref(self.state), s),
+                                                 0.0, C.byref(self.state), s),
                    "dtmpc_general_update")
         _lib.check(self.lib.dtmpc_general_plant(self._dt, C.byref(self.spec), C.byref(self.cfg), self.B,
                                                 self.global_offset, self.t, C.byref(self.state), wp, s),
@@ -352,7 +373,9 @@ class GeneralTubeMPC:
 
     @property
     def loss_mean(self) -> float:
-        return float(self.sums[0]) / self.global_batch
+        """Mean upper loss of the last step over the healthy trajectories of the global batch."""
+        n = float(self.sums[_abi.GEN_SUMS - 1])
+        return float(self.sums[0]) / n if n > 0 else float("nan")
 
 
 def _save_outputs(run_dir: str, traj: ExperimentTrajectories) -> None:

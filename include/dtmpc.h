@@ -33,13 +33,15 @@
 extern "C" {
 #endif
 
-#define DTMPC_ABI_VERSION 2
+#define DTMPC_ABI_VERSION 3
 #define DTMPC_MAX_OBS 16
 #define DTMPC_MAX_ALPHAS 8
 #define DTMPC_MAX_HORIZON 512
 #define DTMPC_LOG_FIELDS 18 /* rows of dtmpc_tube_state.log */
 #define DTMPC_GEN_LOG_FIELDS 12 /* rows of dtmpc_general_state.log */
-#define DTMPC_GEN_SUMS 24 /* L, ancillary raw-theta grads (11), nominal raw-theta-bar grads (12) */
+#define DTMPC_GEN_SUMS 25 /* L, ancillary raw-theta grads (11), nominal raw-theta-bar grads (12),
+                             healthy-trajectory count */
+#define DTMPC_TUBE_SUMS 8 /* L, gQ(3), gR(2), gqb, healthy-trajectory count */
 
 /* scalar type of the arrays */
 enum { DTMPC_F32 = 0, DTMPC_F64 = 1 };
@@ -153,12 +155,16 @@ typedef struct dtmpc_tube_state {
   void* Uaux;       /* [N][2][B]  in: ancillary warm start, out: shifted warm start */
   void* work;       /* dtmpc_tube_workspace_bytes() scratch */
   const void* theta;/* [6] ancillary weights Qa(3), Ra(2), qba (shared by the batch) */
-  void* partials;   /* [nblocks][8] per-workgroup sums: L, gQ(3), gR(2), gqb, pad */
+  void* partials;   /* [n_partials][8] per-workgroup sums over the HEALTHY trajectories (status 0
+                       after this step): L, gQ(3), gR(2), gqb, and their count */
   void* log;        /* [18][B] or NULL: x(3) u(2) xbar(3) ubar(2) b L gQ(3) gR(2) gqb of step t
                        (the gradient rows are the trajectory's own contribution before any
                        status masking) */
   int32_t* status;  /* [B] DTMPC_ST_* bits (OR-accumulated) */
   int32_t* iters;   /* [2][B] nominal / ancillary iterations used, or NULL */
+  int32_t lanes;    /* lanes per trajectory, fixed when the state is built: dtmpc_tube_lanes(B) */
+  int32_t pad_;
+  int64_t n_partials; /* rows of `partials`; must be >= dtmpc_tube_partials_count(B, lanes) */
 } dtmpc_tube_state;
 
 int dtmpc_abi_version(void);
@@ -228,8 +234,14 @@ int dtmpc_doc_grad(int dtype, int32_t horizon, int64_t B, const void* Xaux, cons
 
 /* Scratch bytes for dtmpc_tube_step. */
 size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B);
-/* Number of per-workgroup partial records dtmpc_tube_step writes for a batch of B. */
-int64_t dtmpc_tube_partials_count(int64_t B);
+/* Lanes per trajectory the fused step uses for a batch of B: 1 above 16,384 trajectories (one wave
+ * per SIMD at the benchmark batch), 2 below (paired line search); the environment variable
+ * DTMPC_TUBE_LANES=1|2 overrides.  Resolved ONCE, when the caller builds its state
+ * (dtmpc_tube_state.lanes); dtmpc_tube_step never reads the environment. */
+int32_t dtmpc_tube_lanes(int64_t B);
+/* Number of per-workgroup partial records dtmpc_tube_step writes for B trajectories at `lanes`
+ * lanes per trajectory (0 if lanes is not a supported count). */
+int64_t dtmpc_tube_partials_count(int64_t B, int32_t lanes);
 
 /* One closed-loop step for every trajectory (core/tube_mpc.py:803-1023 loop body):
  *   nominal iLQR -> ancillary iLQR tracking it -> upper loss -> sensitivity -> DOC gradient
@@ -242,12 +254,15 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
                     int64_t global_offset, int64_t step, const dtmpc_tube_state* state,
                     const void* w, void* stream);
 
-/* Fixed-order sum of the per-workgroup partial records: sums [8] (L, gQ(3), gR(2), gqb, 0). */
+/* Fixed-order sum of the per-workgroup partial records: sums [8] (L, gQ(3), gR(2), gqb, count). */
 int dtmpc_partials_reduce(int dtype, int64_t n_partials, const void* partials, void* sums,
                           void* stream);
 
 /* Momentum + projected update of the shared ancillary weights (core/tube_mpc.py:978-984) with
- * the batch-mean gradient g = sums[1:7] * inv_batch.  theta [6] and velocity [6] in/out. */
+ * the batch-mean gradient g = sums[1:7] * inv_batch, or, for inv_batch <= 0, the mean over the
+ * healthy trajectories g = sums[1:7] / sums[7] (g = 0 when none is healthy: a flagged trajectory
+ * -- the reference raises there -- drops out of the mean instead of pulling it toward zero).
+ * theta [6] and velocity [6] in/out. */
 int dtmpc_theta_update(int dtype, const dtmpc_adapt_cfg* cfg, double inv_batch, const void* sums,
                        void* theta, void* velocity, void* stream);
 
@@ -334,21 +349,26 @@ typedef struct dtmpc_general_state {
   void* theta;      /* [2][12] raw parameters, row 0 ancillary theta, row 1 nominal theta-bar
                        (shared by the batch; updated in place by dtmpc_general_update) */
   void* velocity;   /* [2][12] momentum buffers */
-  void* partials;   /* [nblocks][24] per-workgroup sums */
-  void* sums;       /* [24] batch sums (after the cross-rank all-reduce) */
-  void* gout;       /* [24][B] or NULL: each trajectory's own L and raw gradients */
+  void* partials;   /* [n_partials][25] per-workgroup sums over the healthy trajectories */
+  void* sums;       /* [25] batch sums (after the cross-rank all-reduce) */
+  void* gout;       /* [25][B] or NULL: each trajectory's own L (always) and raw gradients
+                       (0 for a flagged trajectory), row 24 = 1 if healthy */
   void* log;        /* [12][B] or NULL: x(3) u(2) xbar(3) ubar(2) b L of step t */
   int32_t* status;  /* [B] */
   int32_t* iters;   /* [2][B] or NULL */
+  int64_t n_partials; /* rows of `partials`; must be >= dtmpc_general_partials_count(B) */
 } dtmpc_general_state;
 
 size_t dtmpc_general_workspace_bytes(int dtype, int32_t horizon, int64_t B);
+/* Number of per-workgroup partial records dtmpc_general_step writes (one lane per trajectory). */
+int64_t dtmpc_general_partials_count(int64_t B);
 
 /* Solves + sensitivities + IFT gradients for every trajectory (core/tube_mpc.py:217-584):
  * nominal iLQR with theta-bar -> ancillary iLQR tracking it with theta -> upper loss ->
  * ancillary sensitivity -> ancillary IFT (theta, X_ref, U_ref) -> [adapt_nominal] nominal
  * sensitivity driven by the reference gradients -> nominal IFT (theta-bar); per-workgroup sums of
- * [L, g_theta(11), g_theta_bar(12)] into state->partials.  theta is read only. */
+ * [L, g_theta(11), g_theta_bar(12), count] over the healthy trajectories into state->partials.
+ * theta is read only. */
 int dtmpc_general_step(int dtype, const dtmpc_spec* spec, const dtmpc_general_cfg* cfg, int64_t B,
                        const dtmpc_general_state* state, void* stream);
 
@@ -357,7 +377,8 @@ int dtmpc_partials_reduce_n(int dtype, int64_t n_partials, int32_t width, const 
                             void* sums, void* stream);
 
 /* Momentum / clipped / projected update of theta and theta-bar with the batch-mean gradient
- * g = state->sums * inv_batch (core/tube_mpc.py:239-255, 507-508, 584). */
+ * g = state->sums * inv_batch, or for inv_batch <= 0 the healthy-trajectory mean
+ * g = state->sums / state->sums[24] (core/tube_mpc.py:239-255, 507-508, 584). */
 int dtmpc_general_update(int dtype, const dtmpc_spec* spec, const dtmpc_general_cfg* cfg,
                          double inv_batch, const dtmpc_general_state* state, void* stream);
 

@@ -230,10 +230,11 @@ class Oracle:
 
     def general_step(self, spec, gcfg, st: dict, theta):
         """Solves + sensitivities + IFT for every trajectory; `st` SoA numpy arrays as tube_step.
-        theta [2, 12] raw.  Returns gout [24, B], status [B], iters [2, B]."""
+        theta [2, 12] raw.  Returns gout [25, B] (L, 11 + 12 raw gradients, healthy flag), status [B],
+        iters [2, B]."""
         B = st["b"].shape[0]
         theta = np.ascontiguousarray(self._a(theta).reshape(2, 12))
-        gout = np.zeros((24, B), self.dt)
+        gout = np.zeros((25, B), self.dt)
         status = np.zeros(B, np.int32)
         iters = np.zeros((2, B), np.int32)
         for k in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux"):

@@ -352,7 +352,10 @@ void FN(oracle_general_step)(const dtmpc_spec* sp, const dtmpc_general_cfg* cfg,
       FN(scatter)(Vn, N, 2, B, i, Unom);
       FN(scatter)(Xa, N + 1, 4, B, i, Xaux);
       FN(scatter)(Va, N, 2, B, i, Uaux);
-      for (int j = 0; j < DTMPC_GEN_SUMS; ++j) gout[(long long)j * B + i] = st ? (REAL)0 : go[j];
+      /* L always (logged); gradients zero and healthy count 0 for a flagged trajectory */
+      go[DTMPC_GEN_SUMS - 1] = 1;
+      gout[i] = go[0];
+      for (int j = 1; j < DTMPC_GEN_SUMS; ++j) gout[(long long)j * B + i] = st ? (REAL)0 : go[j];
       if (status) status[i] |= st;
       if (iters) {
         iters[i] = itn;
@@ -406,6 +409,7 @@ static void FN(apply_update)(const dtmpc_general_cfg* cfg, REAL inv_batch, const
 void FN(oracle_general_update)(const dtmpc_spec* sp, const dtmpc_general_cfg* cfg, double inv_batch,
                                const REAL* sums, REAL* theta, REAL* vel) {
   REAL ib = (REAL)inv_batch;
+  if (!(inv_batch > 0)) ib = sums[DTMPC_GEN_SUMS - 1] > 0 ? (REAL)1 / sums[DTMPC_GEN_SUMS - 1] : (REAL)0;
   int alpha_used = sp->barrier_type != DTMPC_BARRIER_LOG;
   if (cfg->adapt_ancillary) {
     const REAL* g = sums + 1;

@@ -1090,12 +1090,15 @@ void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long 
   }
 }
 
-/* momentum + projected update core/tube_mpc.py:978-984 with g = sums[1:7] * inv_batch */
+/* momentum + projected update core/tube_mpc.py:978-984 with g = sums[1:7] * inv_batch, or for
+ * inv_batch <= 0 the mean over the healthy trajectories counted in sums[7] (dtmpc_theta_update) */
 void FN(oracle_theta_update)(const dtmpc_adapt_cfg* cfg, double inv_batch, const REAL* sums,
                              REAL* theta, REAL* vel) {
   REAL mom = (REAL)cfg->momentum, eta = (REAL)cfg->lr_eta;
+  REAL ib = (REAL)inv_batch;
+  if (!(inv_batch > 0)) ib = sums[7] > 0 ? (REAL)1 / sums[7] : (REAL)0;
   for (int j = 0; j < 6; ++j) {
-    REAL g = sums[1 + j] * (REAL)inv_batch;
+    REAL g = sums[1 + j] * ib;
     vel[j] = mom * vel[j] + g;
     REAL t = theta[j] - eta * vel[j];
     if (j < 3) {

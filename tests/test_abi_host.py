@@ -114,7 +114,21 @@ def test_arguments_validated_before_any_device_call(lib):
     rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
     assert rc == _abi.ERR_BAD_ARG and b"same width" in lib.dtmpc_last_error()
     assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536) == 4 * 50 * 30 * 65536  # SoA scratch 20 + AoS gains 10
-    assert lib.dtmpc_tube_partials_count(65536) == 256
+    assert lib.dtmpc_tube_partials_count(65536, 1) == 256
+    assert lib.dtmpc_tube_partials_count(1000, 2) == 8
+    assert lib.dtmpc_tube_partials_count(1000, 3) == 0
+    assert lib.dtmpc_general_partials_count(1000) == 4
+    assert lib.dtmpc_tube_lanes(65536) in (1, 2) and lib.dtmpc_tube_lanes(4096) in (1, 2)
+    # the lane count and the partials size come from the state (resolved once by the caller)
+    tc.aux_ilqr = st.ilqr_aux.to_c()
+    for f in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux", "work", "theta", "partials", "status"):
+        setattr(state, f, 1)
+    state.lanes, state.n_partials = 3, 1
+    rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
+    assert rc == _abi.ERR_BAD_ARG and b"lanes" in lib.dtmpc_last_error()
+    state.lanes, state.n_partials = 2, 0
+    rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
+    assert rc == _abi.ERR_BAD_ARG and b"n_partials" in lib.dtmpc_last_error()
     assert lib.dtmpc_sensitivity_workspace_bytes(_abi.F64, 50, 10, 1) == 8 * 10 * (50 * 20 + 51 * 20)
 
 

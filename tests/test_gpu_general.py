@@ -152,7 +152,9 @@ def test_general_step_batched_vs_oracle(dev, oracle_lib, tag):
         assert frac >= need, (t, "gout", frac, np.sort(e)[-5:])
         # theta update on the device's own (masked) batch sums
         sums = gdev.astype(np.float64).sum(1).astype(npdt)
-        th_ref, vel_ref = ors[0].general_update(sp, gc, 1.0 / B, sums, th0, vel0)
+        assert sums[-1] == (mpc.status.cpu().numpy() == 0).sum()  # healthy count (last gout row)
+        # inv_batch 0: the mean over the healthy trajectories, as GeneralTubeMPC.step asks for
+        th_ref, vel_ref = ors[0].general_update(sp, gc, 0.0, sums, th0, vel0)
         th = mpc.theta.cpu().numpy()
         tol = 1e-10 if tag == "f64" else 2e-5
         assert np.allclose(th, th_ref, rtol=tol, atol=tol * 0.05 * (np.abs(vel_ref) + 1)), (t, th - th_ref)

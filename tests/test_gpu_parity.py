@@ -404,10 +404,14 @@ def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode, lanes, monkeypatch):
         # with the oracle's theta instead would be a lottery: the batch mean is dominated by the few
         # obstacle-grazing trajectories whose gradients are chaotic -- the three CPU builds' thetas
         # already differ by up to 3e4 relative on this batch.)
-        g = np.where(mpc.status.cpu().numpy() == 0, log[11:18], 0).astype(np.float64)
+        healthy = mpc.status.cpu().numpy() == 0
+        g = np.where(healthy, log[11:18], 0).astype(np.float64)
         sums = np.zeros(8)
         sums[:7] = g.sum(1)
-        th_ref, _ = ors[0].theta_update(st.adapt.to_c(), 1.0 / B, sums.astype(npdt), th0, vel0)
+        sums[7] = healthy.sum()
+        assert int(round(float(mpc.sums[7]))) == int(healthy.sum())  # the device's healthy count
+        # inv_batch 0: the mean over the healthy trajectories, as TubeMPC.step asks the device for
+        th_ref, _ = ors[0].theta_update(st.adapt.to_c(), 0.0, sums.astype(npdt), th0, vel0)
         th = mpc.theta.cpu().numpy()
         eta = st.adapt.lr_eta
         scale = np.abs(th0) + eta * (np.abs(vel0) + np.abs(g).sum(1)[1:] / B) + 1e-30
