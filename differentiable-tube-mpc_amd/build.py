@@ -11,9 +11,10 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRCS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_kernels.hip", "dtmpc_general.hip", "dtmpc_receding.hip")]
+SRCS = [os.path.join(HERE, "csrc", f)
+        for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_general.hip", "dtmpc_receding.hip")]
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solver.hpp", "dtmpc_general.hpp",
-                                                 "dtmpc_host.hpp")] + [
+                                                 "dtmpc_host.hpp", "dtmpc_ls_pk.hpp")] + [
     os.path.join(os.path.dirname(HERE), "include", "dtmpc.h")
 ]
 OUT = os.path.join(HERE, "diff_tube_mpc_strict_pt", "libdtmpc.so")

@@ -1,0 +1,1167 @@
+// dtmpc_fast.hip — the closed-loop tube step specialised for the paper problem (gfx950, f32).
+//
+// Same algorithm, same operations and -- in every forward pass -- the same IEEE rounding as
+// tube_step_kernel (dtmpc_kernels.hip) on the configuration the benchmark and the paper run:
+// smooth-min obstacles (compile-time count M <= 8), the relaxed inverse barrier, an untightened h,
+// a fixed target-tracking nominal cost without angle wrap, an ancillary tracking cost, and six
+// rolled-out line-search candidates (seven alphas, one of them 0).  Everything the generic kernel
+// decides at run time inside its step loops (obstacle aggregation and count, barrier kind, cost
+// kind, wrapped targets, lane count) is fixed here, so its loops are straight-line code with the
+// problem constants in scalar registers, and every tape access is one global load/store with a
+// scalar plane base and a fixed per-lane byte offset (no per-access address arithmetic).
+//
+// Lanes per trajectory P (1 or 2).  P = 1: one lane runs the trajectory (all six candidates as
+// three packed pairs).  P = 2: two adjacent lanes run it; each rolls out three of the six
+// line-search candidates (one packed pair + one single) and the pair agrees on the winner through one
+// DPP lane swap; the rest (backward pass, commit, sensitivity, plant) is computed by both lanes.
+// With P = 2 a batch has twice the waves: two waves per SIMD at the benchmark batch, so one
+// wave's memory waits and dependency stalls hide behind the other's issue.
+//
+// Reference: core/tube_mpc.py:803-1023 (loop body), core/ddp.py:102-307 (iLQR), :317-427
+// (sensitivity), core/tube_mpc.py:915-984 (upper loss, DOC gradient, update).
+#include <hip/hip_runtime.h>
+
+#include "../../include/dtmpc.h"
+#include "dtmpc_host.hpp"
+#include "dtmpc_ls_pk.hpp"
+
+namespace dtmpc {
+namespace fk {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int NC = 6;  // rolled-out line-search candidates (alpha = 0 is the current tape)
+
+// Uniform problem constants (kernarg).  a = max(alpha, eps) and its powers are formed on the host in
+// f32 exactly as the generic kernel forms them on the device (1/a and 1/a^2 correctly rounded).
+struct FP {
+  int N;
+  float dt, umin0, umin1, umax0, umax1, active_tol;
+  float neg_beta, neg_inv_beta;
+  float a, eps, gamma, inv_a, a2, a3, inv_a2;
+  float cx[8], cy[8], r2[8];
+};
+
+struct FCost {  // nominal: target; ancillary: tracking (terminal weight = stage weight)
+  float Q0, Q1, Q2, R0, R1, Qf0, Qf1, Qf2, qb, t0, t1, t2;
+};
+
+struct FIlqr {
+  int max_iter, zpos;
+  float tol, reg;
+  float cal[NC];
+  int cpos[NC];
+};
+
+struct FArgs {
+  int B;
+  long long goff, step;
+  float* x;
+  float* b;
+  float* xbar;
+  float* bbar;
+  float* Xnom;
+  float* Unom;
+  float* Xaux;
+  float* Uaux;
+  float* gK;   // [N][B][8] iLQR / sensitivity gains K
+  float* gk;   // [N][B][2] k
+  float* ab8;  // [N][B][8] sensitivity: a02 a12 a30 a31 a32 b00 b10 b30
+  float* ab2;  // [N][B][2] b31, active set
+  const float* theta;
+  float* partials;
+  float* log;
+  int* status;
+  int* iters;
+  const float* w;
+  int disturbance, write_log;
+  unsigned long long seed;
+  float wlo[3], whi[3];
+};
+
+// ---------------------------------------------------------------------------------------------
+// memory access.  Every tape access is ONE global load / store in the scalar-base form
+// (global_load v, v_off, s[base:base+1]): the row base is uniform (kept in SGPRs: the empty asm
+// stops the compiler from folding the per-lane offset into a 64-bit per-lane VGPR address, which
+// costs a 64-bit VALU multiply-add per access), the per-lane part a 32-bit byte offset fixed for
+// the whole kernel.
+typedef __attribute__((address_space(1))) char gchar;
+__device__ __forceinline__ float* gaddr(const char* base, size_t row_off, unsigned lane_off) {
+  gchar* row = (gchar*)base + row_off;
+  __asm__("" : "+s"(row));
+  // the lane offset is re-materialised here (volatile: not hoisted out of the step loop), so the
+  // zero-extension and the add stay in the access's block and select the scalar-base form
+  __asm__ volatile("" : "+v"(lane_off));
+  return (float*)(row + lane_off);
+}
+
+// per-lane byte offsets of field f of a SoA row: trajectory * 4 + f * B * 4 (four VGPRs shared by
+// every SoA tape of the batch)
+struct Lane {
+  unsigned f0, f1, f2, f3;
+};
+
+// SoA [rows][F][B] f32 array (the ABI tapes): element (k, f) of this lane (f a compile-time constant)
+template <int F>
+struct Soa {
+  char* base;
+  unsigned rs;  // F * B * 4
+  Lane L;
+  __device__ __forceinline__ float* p(int k, int f) const {
+    const unsigned o = f == 0 ? L.f0 : f == 1 ? L.f1 : f == 2 ? L.f2 : L.f3;
+    return gaddr(base, (size_t)(unsigned)k * rs, o);
+  }
+  __device__ __forceinline__ float ld(int k, int f) const { return *p(k, f); }
+  __device__ __forceinline__ void st(int k, int f, float v) const { *p(k, f) = v; }
+};
+
+// per-lane records [rows][B][W] f32 (W = 2 or 8): row k of this lane
+template <int W>
+struct Rec {
+  char* base;
+  unsigned rs;  // B * W * 4
+  unsigned lo;  // trajectory * W * 4
+  __device__ __forceinline__ float* p(int k) const {
+    return gaddr(base, (size_t)(unsigned)k * rs, lo);
+  }
+};
+
+__device__ __forceinline__ f4 ld4(const float* q) { return *(const f4*)__builtin_assume_aligned(q, 16); }
+__device__ __forceinline__ f2 ld2(const float* q) { return *(const f2*)__builtin_assume_aligned(q, 8); }
+__device__ __forceinline__ void st4(float* q, f4 v) { *(f4*)__builtin_assume_aligned(q, 16) = v; }
+__device__ __forceinline__ void st2(float* q, f2 v) { *(f2*)__builtin_assume_aligned(q, 8) = v; }
+
+struct Gains {
+  Rec<8> K;
+  Rec<2> k;
+  __device__ __forceinline__ void store(int s, const float* Kk, const float* kk) const {
+    float* q = K.p(s);
+    st4(q, f4{Kk[0], Kk[1], Kk[2], Kk[3]});
+    st4(q + 4, f4{Kk[4], Kk[5], Kk[6], Kk[7]});
+    st2(k.p(s), f2{kk[0], kk[1]});
+  }
+};
+
+// the lane pair's partner value (P = 2): DPP quad_perm [1, 0, 3, 2], one VALU move
+__device__ __forceinline__ float pswap(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ int pswap(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+
+// ---------------------------------------------------------------------------------------------
+// elementwise math on V = float (one candidate) or f2 (a candidate pair, packed f32 VALU)
+
+template <class V> struct VT;
+template <> struct VT<float> { static constexpr int W = 1; };
+template <> struct VT<f2> { static constexpr int W = 2; };
+
+__device__ __forceinline__ float vmin(float a, float b) { return m_min(a, b); }
+__device__ __forceinline__ f2 vmin(f2 a, f2 b) { return f2{m_min(a.x, b.x), m_min(a.y, b.y)}; }
+__device__ __forceinline__ float vclamp(float v, float lo, float hi) { return clampv(v, lo, hi); }
+__device__ __forceinline__ f2 vclamp(f2 v, float lo, float hi) { return f2{clampv(v.x, lo, hi), clampv(v.y, lo, hi)}; }
+__device__ __forceinline__ float vexp(float x) { return m_exp(x); }
+__device__ __forceinline__ f2 vexp(f2 x) { return pk_exp(x); }
+__device__ __forceinline__ float vlog(float x) { return m_log(x); }
+__device__ __forceinline__ f2 vlog(f2 x) { return pk_log(x); }
+__device__ __forceinline__ void vsincos(float x, float& s, float& c) { m_sincos(x, &s, &c); }
+__device__ __forceinline__ void vsincos(f2 x, f2& s, f2& c) { pk_sincos(x, s, c); }
+__device__ __forceinline__ bool vfinite(float x) { return finite(x); }
+__device__ __forceinline__ bool vfinite(f2 x) { return finite(x.x) && finite(x.y); }
+
+// relaxed inverse barrier B_alpha (core/barrier.py:36-59) as barrier_relaxed (dtmpc_device.hpp):
+// 1 / max(z, eps) for z >= a; the quadratic extension below a (rare: a trajectory inside an
+// obstacle's margin) is a divergent branch the wave skips when no lane needs it
+__device__ __forceinline__ float bar_relaxed(const FP& p, float z) {
+  DTMPC_NOCONTRACT
+  const float diff = z - p.a;
+  return (p.inv_a - diff / p.a2) + (diff * diff) / p.a3;
+}
+__device__ __forceinline__ float vbarrier(const FP& p, float z) {
+  DTMPC_NOCONTRACT
+  float r = m_rcp(z < p.eps ? p.eps : z);
+  if (!(z >= p.a)) r = bar_relaxed(p, z);
+  return r;
+}
+__device__ __forceinline__ f2 vbarrier(const FP& p, f2 z) {
+  DTMPC_NOCONTRACT
+  f2 r = f2{m_rcp(z.x < p.eps ? p.eps : z.x), m_rcp(z.y < p.eps ? p.eps : z.y)};
+  if (!(z.x >= p.a) || !(z.y >= p.a)) {
+    if (!(z.x >= p.a)) r.x = bar_relaxed(p, z.x);
+    if (!(z.y >= p.a)) r.y = bar_relaxed(p, z.y);
+  }
+  return r;
+}
+// _dB_relaxed_inv_dz core/systems/dubins_aug_jac.py:31-40 (dbarrier_relaxed)
+__device__ __forceinline__ float dbarrier(const FP& p, float z) {
+  if (z >= p.a) {
+    const float zc = z < p.eps ? p.eps : z;
+    return -m_rcp(zc * zc);
+  }
+  const float diff = z - p.a;
+  return -p.inv_a2 + (2.f * diff) / p.a3;
+}
+
+// smooth-min h (dubins_obstacles.py:41-69), two passes, the h_i of the first kept (h_smoothmin_w)
+template <int M, class V>
+__device__ __forceinline__ V h_sm(const FP& p, V px, V py) {
+  DTMPC_NOCONTRACT
+  V hi[M], hm;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const V dx = px - p.cx[i];
+    const V dy = py - p.cy[i];
+    hi[i] = dx * dx + dy * dy - p.r2[i];
+    hm = i == 0 ? hi[0] : vmin(hm, hi[i]);
+  }
+  const V zmax = p.neg_beta * hm;
+  V se = 0.f;
+#pragma unroll
+  for (int i = 0; i < M; ++i) se += vexp(p.neg_beta * hi[i] - zmax);
+  return p.neg_inv_beta * (zmax + vlog(se));
+}
+
+// h and grad h at one point (h_grad_fixed, grad_h_multi_circle_obstacles :72-92)
+template <int M>
+__device__ __forceinline__ float h_grad(const FP& p, float px, float py, float& gx, float& gy) {
+#pragma clang fp contract(off)
+  float z[M], zmax = 0.f;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const float dx = px - p.cx[i];
+    const float dy = py - p.cy[i];
+    z[i] = p.neg_beta * (dx * dx + dy * dy - p.r2[i]);
+    zmax = (i == 0 || z[i] > zmax) ? z[i] : zmax;
+  }
+  float se = 0.f, sx = 0.f, sy = 0.f;
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const float e = m_exp(z[i] - zmax);
+    se += e;
+    sx += e * (2.f * (px - p.cx[i]));
+    sy += e * (2.f * (py - p.cy[i]));
+  }
+  const float inv = m_rcp(se);
+  gx = sx * inv;
+  gy = sy * inv;
+  return p.neg_inv_beta * (zmax + m_log(se));
+}
+
+// DBaS-augmented Dubins step (fhat_vec): x' = dubins_step(x, u) (core/systems/dubins.py:26-45),
+// b' = B(h(x')) - gamma (B(h(x)) - b) (core/barrier.py:75-108); Bc carries B(h(x))
+template <int M, class V>
+__device__ __forceinline__ void fhat(const FP& p, V& x0, V& x1, V& x2, V& b, V u0, V u1, V& Bc) {
+  DTMPC_NOCONTRACT
+  V sn, cs;
+  vsincos(x2, sn, cs);
+  const V dv = p.dt * u0;
+  x0 = x0 + dv * cs;
+  x1 = x1 + dv * sn;
+  x2 = x2 + p.dt * u1;
+  const V Bn = vbarrier(p, h_sm<M>(p, x0, x1));
+  b = Bn - p.gamma * (Bc - b);
+  Bc = Bn;
+}
+
+template <int M>
+__device__ __forceinline__ float barrier_at(const FP& p, float px, float py) {
+  return vbarrier(p, h_sm<M>(p, px, py));
+}
+
+// stage / terminal cost (stage_cost / term_cost, core/tube_mpc.py:823-842, 875-894): TRACK takes the
+// references r (state) and q (control), the nominal its fixed target
+template <bool TRACK, class V>
+__device__ __forceinline__ V stage(const FCost& c, V x0, V x1, V x2, V b, V u0, V u1, float r0, float r1, float r2,
+                                   float q0, float q1) {
+  DTMPC_NOCONTRACT
+  V d0, d1, d2, e0, e1;
+  if (TRACK) {
+    d0 = x0 - r0;
+    d1 = x1 - r1;
+    d2 = x2 - r2;
+    e0 = u0 - q0;
+    e1 = u1 - q1;
+  } else {
+    d0 = x0 - c.t0;
+    d1 = x1 - c.t1;
+    d2 = x2 - c.t2;
+    e0 = u0;
+    e1 = u1;
+  }
+  const V sq = c.Q0 * d0 * d0 + c.Q1 * d1 * d1 + c.Q2 * d2 * d2;
+  const V sr = c.R0 * e0 * e0 + c.R1 * e1 * e1;
+  return sq + sr + c.qb * (b * b);
+}
+template <bool TRACK, class V>
+__device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, float r0, float r1, float r2) {
+  DTMPC_NOCONTRACT
+  V d0, d1, d2;
+  if (TRACK) {
+    d0 = x0 - r0;
+    d1 = x1 - r1;
+    d2 = x2 - r2;
+  } else {
+    d0 = x0 - c.t0;
+    d1 = x1 - c.t1;
+    d2 = x2 - c.t2;
+  }
+  const V sq = c.Qf0 * d0 * d0 + c.Qf1 * d1 * d1 + c.Qf2 * d2 * d2;
+  return sq + c.qb * (b * b);
+}
+
+// ---------------------------------------------------------------------------------------------
+// the tapes one iLQR solve works on
+template <bool TRACK>
+struct Solve {
+  Soa<4> X;   // [N+1][4][B] states + barrier state
+  Soa<2> U;   // [N][2][B] controls (in: warm start, out: plan)
+  Soa<4> Xr;  // TRACK: the nominal plan (x, y, theta used)
+  Soa<2> Ur;
+  Gains G;
+};
+
+struct StepIn {
+  float X0, X1, X2, X3, V0, V1, r0, r1, r2, q0, q1;
+  f4 Ka, Kb;
+  f2 kk;
+};
+
+template <bool TRACK>
+__device__ __forceinline__ void load_step(StepIn& L, const Solve<TRACK>& S, int k) {
+  L.X0 = S.X.ld(k, 0);
+  L.X1 = S.X.ld(k, 1);
+  L.X2 = S.X.ld(k, 2);
+  L.X3 = S.X.ld(k, 3);
+  L.V0 = S.U.ld(k, 0);
+  L.V1 = S.U.ld(k, 1);
+  const float* q = S.G.K.p(k);
+  L.Ka = ld4(q);
+  L.Kb = ld4(q + 4);
+  L.kk = ld2(S.G.k.p(k));
+  if (TRACK) {
+    L.r0 = S.Xr.ld(k, 0);
+    L.r1 = S.Xr.ld(k, 1);
+    L.r2 = S.Xr.ld(k, 2);
+    L.q0 = S.Ur.ld(k, 0);
+    L.q1 = S.Ur.ld(k, 1);
+  } else {
+    L.r0 = L.r1 = L.r2 = L.q0 = L.q1 = 0.f;
+  }
+}
+
+// iLQR start (init_tape): V = clamp(V_init), X = rollout(x0, V) and the alpha = 0 candidate's cost
+template <bool TRACK, int M>
+__device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const float* x0, const Solve<TRACK>& S,
+                                           bool want_cost) {
+  DTMPC_NOCONTRACT
+  const int N = p.N;
+  float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3];
+  float Bc = barrier_at<M>(p, x0[0], x0[1]);
+  S.X.st(0, 0, s0);
+  S.X.st(0, 1, s1);
+  S.X.st(0, 2, s2);
+  S.X.st(0, 3, sb);
+  float J = 0.f;
+  float n0 = S.U.ld(0, 0), n1 = S.U.ld(0, 1), nr0 = 0.f, nr1 = 0.f, nr2 = 0.f, nq0 = 0.f, nq1 = 0.f;
+  if (TRACK) {
+    nr0 = S.Xr.ld(0, 0);
+    nr1 = S.Xr.ld(0, 1);
+    nr2 = S.Xr.ld(0, 2);
+    nq0 = S.Ur.ld(0, 0);
+    nq1 = S.Ur.ld(0, 1);
+  }
+  for (int k = 0; k < N; ++k) {
+    const float v0 = n0, v1 = n1, r0 = nr0, r1 = nr1, r2 = nr2, q0 = nq0, q1 = nq1;
+    if (k + 1 < N) {
+      n0 = S.U.ld(k + 1, 0);
+      n1 = S.U.ld(k + 1, 1);
+      if (TRACK) {
+        nr0 = S.Xr.ld(k + 1, 0);
+        nr1 = S.Xr.ld(k + 1, 1);
+        nr2 = S.Xr.ld(k + 1, 2);
+        nq0 = S.Ur.ld(k + 1, 0);
+        nq1 = S.Ur.ld(k + 1, 1);
+      }
+    }
+    const float u0 = clampv(v0, p.umin0, p.umax0), u1 = clampv(v1, p.umin1, p.umax1);
+    S.U.st(k, 0, u0);
+    S.U.st(k, 1, u1);
+    if (want_cost) J = J + stage<TRACK>(c, s0, s1, s2, sb, u0, u1, r0, r1, r2, q0, q1);
+    fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
+    S.X.st(k + 1, 0, s0);
+    S.X.st(k + 1, 1, s1);
+    S.X.st(k + 1, 2, s2);
+    S.X.st(k + 1, 3, sb);
+  }
+  if (!want_cost) return 0.f;
+  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+  if (TRACK) {
+    r0 = S.Xr.ld(N, 0);
+    r1 = S.Xr.ld(N, 1);
+    r2 = S.Xr.ld(N, 2);
+  }
+  return J + term<TRACK>(c, s0, s1, s2, sb, r0, r1, r2);
+}
+
+// sparse augmented Jacobian (make_jac, core/systems/dubins_aug_jac.py:61-139)
+__device__ __forceinline__ Jac<float> jac(const FP& p, float sn, float cs, float v, float gxk, float gyk, float dBk,
+                                          float gxn, float gyn, float dBn) {
+  Jac<float> J;
+  const float dt = p.dt;
+  J.a02 = -dt * v * sn;
+  J.a12 = dt * v * cs;
+  J.b00 = dt * cs;
+  J.b10 = dt * sn;
+  J.b21 = dt;
+  const float r0 = dBn * gxn, r1 = dBn * gyn, r2 = dBn * 0.f;
+  const float gd = p.gamma * dBk;
+  J.a30 = r0 - gd * gxk;
+  J.a31 = r1 - gd * gyk;
+  J.a32 = (r0 * J.a02 + r1 * J.a12 + r2) - gd * 0.f;
+  J.g = p.gamma;
+  J.b30 = r0 * J.b00 + r1 * J.b10;
+  J.b31 = r2 * dt;
+  return J;
+}
+
+// backward pass (ilqr_backward, core/ddp.py:172-254)
+template <bool TRACK, int M>
+__device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg, const Solve<TRACK>& S) {
+  const int N = p.N;
+  const float lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
+  const float luu[2] = {2.f * c.R0, 2.f * c.R1};
+  const float pxx[4] = {2.f * c.Qf0, 2.f * c.Qf1, 2.f * c.Qf2, 2.f * c.qb};
+  const float xn0 = S.X.ld(N, 0), xn1 = S.X.ld(N, 1), xn2 = S.X.ld(N, 2), xnb = S.X.ld(N, 3);
+  float d0, d1, d2;
+  if (TRACK) {
+    d0 = xn0 - S.Xr.ld(N, 0);
+    d1 = xn1 - S.Xr.ld(N, 1);
+    d2 = xn2 - S.Xr.ld(N, 2);
+  } else {
+    d0 = xn0 - c.t0;
+    d1 = xn1 - c.t1;
+    d2 = xn2 - c.t2;
+  }
+  Riccati<float> R;
+  R.Vx[0] = pxx[0] * d0;
+  R.Vx[1] = pxx[1] * d1;
+  R.Vx[2] = pxx[2] * d2;
+  R.Vx[3] = pxx[3] * xnb;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R.Vxx[i][j] = i == j ? pxx[i] : 0.f;
+  float gxn, gyn;
+  float dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
+  bool ok = finite(R.Vx[0]) && finite(R.Vx[1]) && finite(R.Vx[2]) && finite(R.Vx[3]);
+  // step inputs one step ahead
+  float nX0 = S.X.ld(N - 1, 0), nX1 = S.X.ld(N - 1, 1), nX2 = S.X.ld(N - 1, 2), nX3 = S.X.ld(N - 1, 3);
+  float nV0 = S.U.ld(N - 1, 0), nV1 = S.U.ld(N - 1, 1), nr0 = 0.f, nr1 = 0.f, nr2 = 0.f, nq0 = 0.f, nq1 = 0.f;
+  if (TRACK) {
+    nr0 = S.Xr.ld(N - 1, 0);
+    nr1 = S.Xr.ld(N - 1, 1);
+    nr2 = S.Xr.ld(N - 1, 2);
+    nq0 = S.Ur.ld(N - 1, 0);
+    nq1 = S.Ur.ld(N - 1, 1);
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    const float x0 = nX0, x1 = nX1, x2 = nX2, xb = nX3, u0 = nV0, u1 = nV1, r0 = nr0, r1 = nr1, r2 = nr2,
+                q0 = nq0, q1 = nq1;
+    if (k > 0) {
+      nX0 = S.X.ld(k - 1, 0);
+      nX1 = S.X.ld(k - 1, 1);
+      nX2 = S.X.ld(k - 1, 2);
+      nX3 = S.X.ld(k - 1, 3);
+      nV0 = S.U.ld(k - 1, 0);
+      nV1 = S.U.ld(k - 1, 1);
+      if (TRACK) {
+        nr0 = S.Xr.ld(k - 1, 0);
+        nr1 = S.Xr.ld(k - 1, 1);
+        nr2 = S.Xr.ld(k - 1, 2);
+        nq0 = S.Ur.ld(k - 1, 0);
+        nq1 = S.Ur.ld(k - 1, 1);
+      }
+    }
+    float sn, cs;
+    m_sincos(x2, &sn, &cs);
+    float gxk, gyk;
+    const float dBk = dbarrier(p, h_grad<M>(p, x0, x1, gxk, gyk));
+    const Jac<float> J = jac(p, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
+    if (TRACK) {
+      d0 = x0 - r0;
+      d1 = x1 - r1;
+      d2 = x2 - r2;
+    } else {
+      d0 = x0 - c.t0;
+      d1 = x1 - c.t1;
+      d2 = x2 - c.t2;
+    }
+    const float lx[4] = {lxx[0] * d0, lxx[1] * d1, lxx[2] * d2, lxx[3] * xb};
+    float lu[2];
+    if (TRACK) {
+      lu[0] = luu[0] * (u0 - q0);
+      lu[1] = luu[1] * (u1 - q1);
+    } else {
+      lu[0] = luu[0] * u0;
+      lu[1] = luu[1] * u1;
+    }
+    float Kk[8], kk[2];
+    ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
+    S.G.store(k, Kk, kk);
+    gxn = gxk;
+    gyn = gyk;
+    dBn = dBk;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ok = ok && finite(R.Vx[i]);
+  return ok;
+}
+
+// ---------------------------------------------------------------------------------------------
+// line search (core/ddp.py:256-301) over this lane's candidates: NP packed pairs + NS singles
+// (P = 1: the six candidates as three pairs; P = 2: three per lane, one pair + one single), then the
+// first strict minimum over the ORIGINAL candidate order, combined over the lane pair when P = 2,
+// and the alpha = 0 rule (it is the current tape, cost Jprev).  Returns the chosen original position
+// (or -1 if any candidate or Jprev is non-finite), its cost and alpha.
+template <bool TRACK, int M, int P>
+__device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FIlqr& cf, const float* x0, float Bc0,
+                                           const Solve<TRACK>& S, float Jprev, int h, float& bestJ, float& al_out) {
+  DTMPC_NOCONTRACT
+  constexpr int NL = NC / P;       // candidates of this lane
+  constexpr int NP = NL / 2, NS = NL % 2;
+  const int N = p.N;
+  const int c0 = h * NL;           // this lane's first candidate (index into cf.cal / cf.cpos)
+  f2 a0[NP > 0 ? NP : 1], a1[NP > 0 ? NP : 1], a2[NP > 0 ? NP : 1], ab[NP > 0 ? NP : 1], Bp[NP > 0 ? NP : 1],
+      Jp[NP > 0 ? NP : 1], alp[NP > 0 ? NP : 1];
+  float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bs = Bc0, Js = 0.f, als = 0.f;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    a0[q] = x0[0];
+    a1[q] = x0[1];
+    a2[q] = x0[2];
+    ab[q] = x0[3];
+    Bp[q] = Bc0;
+    Jp[q] = 0.f;
+    alp[q] = P == 1 ? f2{cf.cal[2 * q], cf.cal[2 * q + 1]}
+                    : (h ? f2{cf.cal[NL + 2 * q], cf.cal[NL + 2 * q + 1]} : f2{cf.cal[2 * q], cf.cal[2 * q + 1]});
+  }
+  if (NS) als = h ? cf.cal[NL + NL - 1] : cf.cal[NL - 1];
+  StepIn cur, nxt;
+  load_step<TRACK>(nxt, S, 0);
+  for (int k = 0; k < N; ++k) {
+    cur = nxt;
+    if (k + 1 < N) load_step<TRACK>(nxt, S, k + 1);
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const f2 e0 = a0[q] - cur.X0, e1 = a1[q] - cur.X1, e2 = a2[q] - cur.X2, e3 = ab[q] - cur.X3;
+      const f2 du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
+      const f2 du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
+      const f2 u0 = vclamp(cur.V0 + alp[q] * du0, p.umin0, p.umax0);
+      const f2 u1 = vclamp(cur.V1 + alp[q] * du1, p.umin1, p.umax1);
+      Jp[q] = Jp[q] + stage<TRACK>(c, a0[q], a1[q], a2[q], ab[q], u0, u1, cur.r0, cur.r1, cur.r2, cur.q0, cur.q1);
+      fhat<M>(p, a0[q], a1[q], a2[q], ab[q], u0, u1, Bp[q]);
+    }
+    if (NS) {
+      const float e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
+      const float du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
+      const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
+      const float u0 = clampv(cur.V0 + als * du0, p.umin0, p.umax0);
+      const float u1 = clampv(cur.V1 + als * du1, p.umin1, p.umax1);
+      Js = Js + stage<TRACK>(c, s0, s1, s2, sb, u0, u1, cur.r0, cur.r1, cur.r2, cur.q0, cur.q1);
+      fhat<M>(p, s0, s1, s2, sb, u0, u1, Bs);
+    }
+  }
+  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+  if (TRACK) {
+    r0 = S.Xr.ld(N, 0);
+    r1 = S.Xr.ld(N, 1);
+    r2 = S.Xr.ld(N, 2);
+  }
+  float Jc[NL];
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const f2 Jt = Jp[q] + term<TRACK>(c, a0[q], a1[q], a2[q], ab[q], r0, r1, r2);
+    Jc[2 * q] = Jt.x;
+    Jc[2 * q + 1] = Jt.y;
+    ok = ok && vfinite(Jt);
+  }
+  if (NS) {
+    Jc[NL - 1] = Js + term<TRACK>(c, s0, s1, s2, sb, r0, r1, r2);
+    ok = ok && finite(Jc[NL - 1]);
+  }
+  // this lane's first strict minimum (its candidates are in increasing original order)
+  float bJ = Jc[0];
+  int bl = 0;
+#pragma unroll
+  for (int a = 1; a < NL; ++a)
+    if (Jc[a] < bJ) {
+      bJ = Jc[a];
+      bl = a;
+    }
+  int bi = c0 + bl;  // index into the candidate list (its order is the original one)
+  // the zero candidate's neighbours: min over candidates before / after its position
+  float mb = 0.f, ma = 0.f;
+  int hb = 0, ha = 0;
+  if (cf.zpos >= 0) {
+#pragma unroll
+    for (int a = 0; a < NL; ++a) {
+      const int pos = P == 1 ? cf.cpos[a] : (h ? cf.cpos[NL + a] : cf.cpos[a]);
+      if (pos < cf.zpos) {
+        mb = (!hb || Jc[a] < mb) ? Jc[a] : mb;
+        hb = 1;
+      } else {
+        ma = (!ha || Jc[a] < ma) ? Jc[a] : ma;
+        ha = 1;
+      }
+    }
+  }
+  if (P == 2) {  // combine with the partner lane: lexicographic (J, position) = strict <, first wins
+    const float oJ = pswap(bJ);
+    const int oi = pswap(bi);
+    ok = pswap((int)ok) && ok;
+    if (oJ < bJ || (oJ == bJ && oi < bi)) {
+      bJ = oJ;
+      bi = oi;
+    }
+    if (cf.zpos >= 0) {
+      const float omb = pswap(mb), oma = pswap(ma);
+      const int ohb = pswap(hb), oha = pswap(ha);
+      if (ohb) mb = (!hb || omb < mb) ? omb : mb;
+      if (oha) ma = (!ha || oma < ma) ? oma : ma;
+      hb |= ohb;
+      ha |= oha;
+    }
+  }
+  bestJ = bJ;
+  int best = cf.cpos[0];
+  al_out = cf.cal[0];
+#pragma unroll
+  for (int a = 1; a < NC; ++a)
+    if (bi == a) {
+      best = cf.cpos[a];
+      al_out = cf.cal[a];
+    }
+  if (cf.zpos >= 0) {
+    if ((!hb || Jprev < mb) && (!ha || Jprev <= ma)) {
+      best = cf.zpos;
+      bestJ = Jprev;
+      al_out = 0.f;
+    }
+    ok = ok && finite(Jprev);
+  }
+  return ok ? best : -1;
+}
+
+// materialise the chosen candidate in place (commit_candidate): same arithmetic as its lane of the
+// line search; the old X[k+1] is read (prefetched) before it is overwritten
+template <bool TRACK, int M>
+__device__ __forceinline__ void commit(const FP& p, float al, const float* x0, float Bc0, const Solve<TRACK>& S) {
+  DTMPC_NOCONTRACT
+  const int N = p.N;
+  float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bc = Bc0;
+  StepIn cur, nxt;
+  Solve<false> T0;  // no references needed
+  T0.X = S.X;
+  T0.U = S.U;
+  T0.G = S.G;
+  load_step<false>(nxt, T0, 0);
+  for (int k = 0; k < N; ++k) {
+    cur = nxt;
+    if (k + 1 < N) load_step<false>(nxt, T0, k + 1);
+    const float e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
+    const float du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
+    const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
+    const float u0 = clampv(cur.V0 + al * du0, p.umin0, p.umax0);
+    const float u1 = clampv(cur.V1 + al * du1, p.umin1, p.umax1);
+    S.U.st(k, 0, u0);
+    S.U.st(k, 1, u1);
+    fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
+    S.X.st(k + 1, 0, s0);
+    S.X.st(k + 1, 1, s1);
+    S.X.st(k + 1, 2, s2);
+    S.X.st(k + 1, 3, sb);
+  }
+}
+
+// iLQR for one trajectory (ilqr_traj, core/ddp.py:102-307)
+template <bool TRACK, int M, int P>
+__device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const float* x0,
+                                    const Solve<TRACK>& S, int h, int& iters) {
+  float Jcur = init_tape<TRACK, M>(p, c, x0, S, cf.zpos >= 0 && cf.max_iter > 0);
+  const float Bc0 = barrier_at<M>(p, x0[0], x0[1]);
+  bool have_prev = false;
+  float prev = 0.f;
+  iters = 0;
+  for (int it = 0; it < cf.max_iter; ++it) {
+    iters = it + 1;
+    if (!backward<TRACK, M>(p, c, cf.reg, S)) return DTMPC_ST_NONFINITE;
+    float bestJ, al;
+    const int best = line_search<TRACK, M, P>(p, c, cf, x0, Bc0, S, Jcur, h, bestJ, al);
+    if (best < 0) return DTMPC_ST_NONFINITE;
+    if (al != 0.f) commit<TRACK, M>(p, al, x0, Bc0, S);
+    Jcur = bestJ;
+    if (have_prev && m_abs(prev - bestJ) < cf.tol) break;
+    have_prev = true;
+    prev = bestJ;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// DDP sensitivity with the paper upper loss + DOC gradient (sens_traj<float, false, false, true>,
+// core/ddp.py:317-427, core/tube_mpc.py:915-976): acc = L, gQ(3), gR(2), gqb
+template <int M>
+__device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const Solve<true>& S, const Rec<8>& AB8,
+                                           const Rec<2>& AB2, float* acc) {
+  const int N = p.N;
+  const float lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
+  const float luu[2] = {2.f * c.R0, 2.f * c.R1};
+  const float pxx[4] = {2.f * c.Qf0, 2.f * c.Qf1, 2.f * c.Qf2, 2.f * c.qb};
+  const float reg = 1e-9f;
+  Riccati<float> R;  // R.Vx holds tilde V_x
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) R.Vxx[i][j] = i == j ? pxx[i] : 0.f;
+  const float xn0 = S.X.ld(N, 0), xn1 = S.X.ld(N, 1), xnb = S.X.ld(N, 3);
+  R.Vx[0] = 2.f * (xn0 - S.Xr.ld(N, 0));
+  R.Vx[1] = 2.f * (xn1 - S.Xr.ld(N, 1));
+  R.Vx[2] = 2.f * (S.X.ld(N, 2) - S.Xr.ld(N, 2));
+  R.Vx[3] = 2.f * xnb;
+  float gxn, gyn;
+  float dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
+  for (int k = N - 1; k >= 0; --k) {
+    const float x0 = S.X.ld(k, 0), x1 = S.X.ld(k, 1), x2 = S.X.ld(k, 2), xb = S.X.ld(k, 3);
+    const float u0 = S.U.ld(k, 0), u1 = S.U.ld(k, 1);
+    float sn, cs;
+    m_sincos(x2, &sn, &cs);
+    float gxk, gyk;
+    const float dBk = dbarrier(p, h_grad<M>(p, x0, x1, gxk, gyk));
+    const Jac<float> J = jac(p, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
+    gxn = gxk;
+    gyn = gyk;
+    dBn = dBk;
+    float Qxx[4][4], Qxu[4][2], Qux[2][4], Quu[2][2];
+    sens_qblocks(J, R.Vxx, lxx, luu, Qxx, Qxu, Qux, Quu);
+    const float* tv = R.Vx;
+    const float tQu0 = J.b00 * tv[0] + J.b10 * tv[1] + J.b30 * tv[3];
+    const float tQu1 = J.b21 * tv[2] + J.b31 * tv[3];
+    float tQx[4];
+    tQx[0] = 2.f * (x0 - S.Xr.ld(k, 0)) + (tv[0] + J.a30 * tv[3]);
+    tQx[1] = 2.f * (x1 - S.Xr.ld(k, 1)) + (tv[1] + J.a31 * tv[3]);
+    tQx[2] = 2.f * (x2 - S.Xr.ld(k, 2)) + (J.a02 * tv[0] + J.a12 * tv[1] + tv[2] + J.a32 * tv[3]);
+    tQx[3] = 2.f * xb + J.g * tv[3];
+    const bool act0 = (u0 <= p.umin0 + p.active_tol) || (u0 >= p.umax0 - p.active_tol);
+    const bool act1 = (u1 <= p.umin1 + p.active_tol) || (u1 >= p.umax1 - p.active_tol);
+    const float m00 = Quu[0][0] + reg, m11 = Quu[1][1] + reg;
+    const LU2<float> f = lu2(m00, Quu[0][1], Quu[1][0], m11);
+    float Kk[8], kk[2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float y0, y1;
+      solve_reduced(f, m00, m11, act0, act1, Qux[0][j], Qux[1][j], y0, y1);
+      Kk[j] = -y0;
+      Kk[4 + j] = -y1;
+    }
+    {
+      float y0, y1;
+      solve_reduced(f, m00, m11, act0, act1, tQu0, tQu1, y0, y1);
+      kk[0] = -y0;
+      kk[1] = -y1;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      R.Vx[i] = tQx[i] + (Qxu[i][0] * kk[0] + Qxu[i][1] * kk[1]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) R.Vxx[i][j] = Qxx[i][j] + (Qxu[i][0] * Kk[j] + Qxu[i][1] * Kk[4 + j]);
+    }
+    S.G.store(k, Kk, kk);
+    float* q = AB8.p(k);
+    st4(q, f4{J.a02, J.a12, J.a30, J.a31});
+    st4(q + 4, f4{J.a32, J.b00, J.b10, J.b30});
+    st2(AB2.p(k), f2{J.b31, float((act0 ? 1 : 0) + (act1 ? 2 : 0))});
+  }
+  // forward (:413-425) fused with the upper loss and the DOC gradient
+  float d[4] = {0.f, 0.f, 0.f, 0.f};
+  float L1 = 0.f, L2 = 0.f, gQ0 = 0.f, gQ1 = 0.f, gQ2 = 0.f, gR0 = 0.f, gR1 = 0.f, gqb = 0.f;
+  const float g = p.gamma, dt = p.dt;
+  for (int k = 0; k < N; ++k) {
+    const float* gq = S.G.K.p(k);
+    const f4 Ka = ld4(gq), Kb = ld4(gq + 4);
+    const f2 kf = ld2(S.G.k.p(k));
+    const float* q = AB8.p(k);
+    const f4 A0 = ld4(q), A1 = ld4(q + 4);
+    const f2 A2 = ld2(AB2.p(k));
+    const float a02 = A0.x, a12 = A0.y, a30 = A0.z, a31 = A0.w, a32 = A1.x, b00 = A1.y, b10 = A1.z, b30 = A1.w,
+                b31 = A2.x;
+    const int act = (int)A2.y;
+    const float v0 = (act & 1) ? 0.f : kf.x + (Ka.x * d[0] + Ka.y * d[1] + Ka.z * d[2] + Ka.w * d[3]);
+    const float v1 = (act & 2) ? 0.f : kf.y + (Kb.x * d[0] + Kb.y * d[1] + Kb.z * d[2] + Kb.w * d[3]);
+    const float e0 = S.X.ld(k, 0) - S.Xr.ld(k, 0);
+    const float e1 = S.X.ld(k, 1) - S.Xr.ld(k, 1);
+    const float e2 = S.X.ld(k, 2) - S.Xr.ld(k, 2);
+    const float bb = S.X.ld(k, 3);
+    const float w0 = S.U.ld(k, 0) - S.Ur.ld(k, 0);
+    const float w1 = S.U.ld(k, 1) - S.Ur.ld(k, 1);
+    L1 += e0 * e0 + e1 * e1 + e2 * e2;
+    L2 += bb * bb;
+    gQ0 += 2.f * e0 * d[0];
+    gQ1 += 2.f * e1 * d[1];
+    gQ2 += 2.f * e2 * d[2];
+    gR0 += 2.f * w0 * v0;
+    gR1 += 2.f * w1 * v1;
+    gqb += 2.f * bb * d[3];
+    const float n0 = (d[0] + a02 * d[2]) + b00 * v0;
+    const float n1 = (d[1] + a12 * d[2]) + b10 * v0;
+    const float n2 = d[2] + dt * v1;
+    const float n3 = (a30 * d[0] + a31 * d[1] + a32 * d[2] + g * d[3]) + (b30 * v0 + b31 * v1);
+    d[0] = n0;
+    d[1] = n1;
+    d[2] = n2;
+    d[3] = n3;
+  }
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ok = ok && finite(d[i]);
+  const float e0 = S.X.ld(N, 0) - S.Xr.ld(N, 0);
+  const float e1 = S.X.ld(N, 1) - S.Xr.ld(N, 1);
+  const float e2 = S.X.ld(N, 2) - S.Xr.ld(N, 2);
+  const float bb = S.X.ld(N, 3);
+  L1 += e0 * e0 + e1 * e1 + e2 * e2;
+  L2 += bb * bb;
+  acc[0] = L1 + L2;
+  acc[1] = gQ0 + 2.f * e0 * d[0];
+  acc[2] = gQ1 + 2.f * e1 * d[1];
+  acc[3] = gQ2 + 2.f * e2 * d[2];
+  acc[4] = gR0;
+  acc[5] = gR1;
+  acc[6] = gqb + 2.f * bb * d[3];
+  ok = ok && finite(acc[1]) && finite(acc[4]) && finite(acc[5]);
+  return ok ? 0 : DTMPC_ST_NONFINITE;
+}
+
+// ---------------------------------------------------------------------------------------------
+// the fused closed-loop step (tube_step_kernel's body on the fast configuration)
+// All kernel arguments in one struct, passed by value: it sits at offset 0 of the kernarg segment.
+struct FK {
+  FP p;
+  FCost cn;
+  FIlqr cfn, cfa;
+  FArgs a;
+};
+typedef const FK KArg;
+typedef __attribute__((address_space(4))) const FK KArg4;
+
+// The kernel reads its arguments PHASE BY PHASE through this pointer (each call an opaque copy, so
+// the compiler cannot merge the loads of two phases): the constants of one phase -- the nominal
+// solve, the ancillary solve, the sensitivity, the plant -- are loaded into scalar registers when
+// that phase starts and die with it, instead of all of them being loaded at kernel entry and kept
+// live (and spilled) through the whole step.
+__device__ __forceinline__ KArg* kargs() {
+  KArg4* k = (KArg4*)__builtin_amdgcn_kernarg_segment_ptr();
+  __asm__ volatile("" : "+s"(k));
+  return (KArg*)k;  // generic; the compiler infers the constant address space back (scalar loads)
+}
+
+#ifndef DTMPC_FAST_PIN
+#define DTMPC_FAST_PIN 1
+#endif
+// the problem constants of one phase; the obstacle table pinned in VGPRs (every candidate of every
+// step reads it; in scalar registers it is what the compiler would spill first)
+template <int M>
+__device__ __forceinline__ FP phase_p() {
+  FP p = kargs()->p;
+#if DTMPC_FAST_PIN
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    __asm__ volatile("" : "+v"(p.cx[j]));
+    __asm__ volatile("" : "+v"(p.cy[j]));
+    __asm__ volatile("" : "+v"(p.r2[j]));
+  }
+#endif
+  return p;
+}
+
+template <int M, int P>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P, P)))
+tube_fast_kernel(FK kk) {
+  (void)kk;  // read through kargs()
+  __shared__ float red[kBlock / 64][DTMPC_TUBE_SUMS];
+  const int B = kargs()->a.B;
+  const int gl = blockIdx.x * kBlock + threadIdx.x;
+  const int i = P == 1 ? gl : (gl >> 1), h = P == 1 ? 0 : (gl & 1);
+  float acc[DTMPC_TUBE_SUMS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < B) {
+    const size_t nb = (size_t)B;
+    const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
+    const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
+    int st = 0, itn = 0, ita = 0;
+    float x0, x1, x2, xb, y0, y1, y2, yb;
+    {
+      KArg* K = kargs();
+      x0 = K->a.x[i];
+      x1 = K->a.x[nb + i];
+      x2 = K->a.x[2 * nb + i];
+      xb = K->a.b[i];
+      y0 = K->a.xbar[i];
+      y1 = K->a.xbar[nb + i];
+      y2 = K->a.xbar[2 * nb + i];
+      yb = K->a.bbar[i];
+    }
+    {  // nominal MPC (fixed weights, :813-857)
+      KArg* K = kargs();
+      Solve<false> Sn;
+      Sn.X = Soa<4>{(char*)K->a.Xnom, 4u * bb, L};
+      Sn.U = Soa<2>{(char*)K->a.Unom, 2u * bb, L};
+      Sn.G.K = Rec<8>{(char*)K->a.gK, bb * 8u, lo * 8u};
+      Sn.G.k = Rec<2>{(char*)K->a.gk, bb * 2u, lo * 2u};
+      Sn.Xr = Sn.X;
+      Sn.Ur = Sn.U;
+      const FP p = phase_p<M>();
+      const FCost cn = K->cn;
+      const FIlqr cfn = K->cfn;
+      const float xn0[4] = {y0, y1, y2, yb};
+      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, itn);
+    }
+    FCost ca;  // ancillary weights theta (shared by the batch), terminal weight Qa (:885, :891)
+    {
+      const float* th = kargs()->a.theta;
+      ca.Q0 = ca.Qf0 = th[0];
+      ca.Q1 = ca.Qf1 = th[1];
+      ca.Q2 = ca.Qf2 = th[2];
+      ca.R0 = th[3];
+      ca.R1 = th[4];
+      ca.qb = th[5];
+      ca.t0 = ca.t1 = ca.t2 = 0.f;
+    }
+    Solve<true> Sa;
+    {  // ancillary MPC tracking the nominal plan (:863-909)
+      KArg* K = kargs();
+      Sa.X = Soa<4>{(char*)K->a.Xaux, 4u * bb, L};
+      Sa.U = Soa<2>{(char*)K->a.Uaux, 2u * bb, L};
+      Sa.Xr = Soa<4>{(char*)K->a.Xnom, 4u * bb, L};
+      Sa.Ur = Soa<2>{(char*)K->a.Unom, 2u * bb, L};
+      Sa.G.K = Rec<8>{(char*)K->a.gK, bb * 8u, lo * 8u};
+      Sa.G.k = Rec<2>{(char*)K->a.gk, bb * 2u, lo * 2u};
+      const FP p = phase_p<M>();
+      const FIlqr cfa = K->cfa;
+      const float xa0[4] = {x0, x1, x2, xb};
+      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, ita);
+    }
+    {  // upper loss, DOC sensitivity and gradient (:915-976)
+      KArg* K = kargs();
+      const Rec<8> AB8{(char*)K->a.ab8, bb * 8u, lo * 8u};
+      const Rec<2> AB2{(char*)K->a.ab2, bb * 2u, lo * 2u};
+      const FP p = phase_p<M>();
+      st |= sensitivity<M>(p, ca, Sa, AB8, AB2, acc);
+    }
+    {  // plant step with disturbance, nominal propagation (:990-1001), log, warm-start shift
+      KArg* K = kargs();
+      const FArgs& a = K->a;
+      const FP p = phase_p<M>();
+      const Soa<2> Un{(char*)a.Unom, 2u * bb, L}, Ua{(char*)a.Uaux, 2u * bb, L};
+      const float u0 = Ua.ld(0, 0), u1 = Ua.ld(0, 1);
+      const float v0 = Un.ld(0, 0), v1 = Un.ld(0, 1);
+      float w[3];
+      if (a.disturbance == 0) {
+        w[0] = a.w[i];
+        w[1] = a.w[nb + i];
+        w[2] = a.w[2 * nb + i];
+      } else {
+        uint32_t r[4];
+        philox4x32_10(a.seed, (uint64_t)(a.goff + i), (uint64_t)a.step, r);
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+          const float u = float(r[f] >> 8) * float(1.0 / 16777216.0);
+          w[f] = a.wlo[f] + (a.whi[f] - a.wlo[f]) * u;
+        }
+      }
+      if (a.write_log && h == 0) {
+        float* lg = a.log;
+        lg[i] = x0;
+        lg[nb + i] = x1;
+        lg[2 * nb + i] = x2;
+        lg[3 * nb + i] = u0;
+        lg[4 * nb + i] = u1;
+        lg[5 * nb + i] = y0;
+        lg[6 * nb + i] = y1;
+        lg[7 * nb + i] = y2;
+        lg[8 * nb + i] = v0;
+        lg[9 * nb + i] = v1;
+        lg[10 * nb + i] = xb;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) lg[(11 + j) * nb + i] = acc[j];
+      }
+      {
+        float q0 = x0, q1 = x1, q2 = x2, qb = xb, Bc = barrier_at<M>(p, x0, x1);
+        fhat<M>(p, q0, q1, q2, qb, u0, u1, Bc);
+        a.x[i] = q0 + w[0];
+        a.x[nb + i] = q1 + w[1];
+        a.x[2 * nb + i] = q2 + w[2];
+        a.b[i] = qb;
+      }
+      {
+        float q0 = y0, q1 = y1, q2 = y2, qb = yb, Bc = barrier_at<M>(p, y0, y1);
+        fhat<M>(p, q0, q1, q2, qb, v0, v1, Bc);
+        a.xbar[i] = q0;
+        a.xbar[nb + i] = q1;
+        a.xbar[2 * nb + i] = q2;
+        a.bbar[i] = qb;
+      }
+      // warm-start shift V <- [V[1:], V[-1]]  (:1015-1020)
+      for (int k = 0; k + 1 < p.N; ++k) {
+        Un.st(k, 0, Un.ld(k + 1, 0));
+        Un.st(k, 1, Un.ld(k + 1, 1));
+        Ua.st(k, 0, Ua.ld(k + 1, 0));
+        Ua.st(k, 1, Ua.ld(k + 1, 1));
+      }
+      acc[7] = 1.f;
+      if (st || h != 0) {  // healthy trajectories only; a lane pair counts once
+#pragma unroll
+        for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) acc[j] = 0.f;
+      }
+      if (h == 0) {
+        a.status[i] |= st;
+        if (a.iters) {
+          a.iters[i] = itn;
+          a.iters[nb + i] = ita;
+        }
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) {
+    const float v = wave_sum(acc[j]);
+    if (lane == 0) red[wv][j] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < DTMPC_TUBE_SUMS) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < kBlock / 64; ++q) v += red[q][threadIdx.x];
+    kargs()->a.partials[(size_t)blockIdx.x * DTMPC_TUBE_SUMS + threadIdx.x] = v;
+  }
+}
+
+}  // namespace fk
+
+// ---------------------------------------------------------------------------------------------
+// host side
+
+// The fast kernel's configuration: f32, smooth-min over 1..8 obstacles, relaxed inverse barrier,
+// untightened h, nominal target cost without wrap, and six rolled-out candidates in both solves.
+// DTMPC_FAST=0 (environment, read at the call) forces the generic kernel (parity tests compare both).
+bool tube_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf) {
+  const char* e = getenv("DTMPC_FAST");
+  if (e && e[0] == '0' && e[1] == 0) return false;
+  if (dtype != DTMPC_F32) return false;
+  if (sp->obs_aggregation != DTMPC_OBS_SMOOTHMIN || sp->n_obstacles < 1 || sp->n_obstacles > 8) return false;
+  if (sp->barrier_type != DTMPC_BARRIER_INVERSE || sp->h_offset != 0.0) return false;
+  if (cf->nominal.kind != DTMPC_COST_TARGET || cf->nominal.wrap_angle) return false;
+  const DIlqr<float> n = make_ilqr<float>(cf->nom_ilqr), a = make_ilqr<float>(cf->aux_ilqr);
+  return n.nc == fk::NC && a.nc == fk::NC;
+}
+
+static fk::FIlqr fast_ilqr(const dtmpc_ilqr_cfg& c) {
+  const DIlqr<float> d = make_ilqr<float>(c);
+  fk::FIlqr o;
+  o.max_iter = d.max_iter;
+  o.zpos = d.zpos;
+  o.tol = d.tol;
+  o.reg = d.reg;
+  for (int q = 0; q < fk::NC; ++q) {
+    o.cal[q] = d.calphas[q];
+    o.cpos[q] = d.cpos[q];
+  }
+  return o;
+}
+
+int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
+                     const dtmpc_tube_state* S, const void* w, hipStream_t st) {
+  fk::FK kk;
+  std::memset(&kk, 0, sizeof(kk));
+  fk::FP& p = kk.p;
+  const DSpec<float> s = make_spec<float>(*sp);
+  p.N = s.N;
+  p.dt = s.dt;
+  p.umin0 = s.umin0;
+  p.umin1 = s.umin1;
+  p.umax0 = s.umax0;
+  p.umax1 = s.umax1;
+  p.active_tol = s.active_tol;
+  p.neg_beta = s.neg_beta;
+  p.neg_inv_beta = s.neg_inv_beta;
+  p.eps = s.eps;
+  p.gamma = s.gamma;
+  // alpha_eff = max(alpha, eps) and the constants of the relaxed branch, in f32 as the device forms them
+  p.a = s.alpha > s.eps ? s.alpha : s.eps;
+  p.a2 = p.a * p.a;
+  p.a3 = p.a2 * p.a;
+  volatile float one = 1.0f;  // f32 division on the host: correctly rounded, as the device's
+  p.inv_a = one / p.a;
+  p.inv_a2 = one / p.a2;
+  for (int i = 0; i < 8; ++i) {
+    p.cx[i] = i < s.M ? s.cx[i] : 0.f;
+    p.cy[i] = i < s.M ? s.cy[i] : 0.f;
+    p.r2[i] = i < s.M ? s.r2[i] : 0.f;
+  }
+  const DCost<float> c = make_cost<float>(cf->nominal);
+  kk.cn = fk::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb, c.t0, c.t1, c.t2};
+  kk.cfn = fast_ilqr(cf->nom_ilqr);
+  kk.cfa = fast_ilqr(cf->aux_ilqr);
+  fk::FArgs& a = kk.a;
+  const int N = sp->horizon;
+  a.B = (int)B;
+  a.goff = goff;
+  a.step = step;
+  a.x = (float*)S->x;
+  a.b = (float*)S->b;
+  a.xbar = (float*)S->xbar;
+  a.bbar = (float*)S->bbar;
+  a.Xnom = (float*)S->Xnom;
+  a.Unom = (float*)S->Unom;
+  a.Xaux = (float*)S->Xaux;
+  a.Uaux = (float*)S->Uaux;
+  float* wk = (float*)S->work;  // 20 N B of the 30 N B floats of dtmpc_tube_workspace_bytes
+  const size_t nb = (size_t)B * N;
+  a.gK = wk;
+  a.gk = wk + 8 * nb;
+  a.ab8 = wk + 10 * nb;
+  a.ab2 = wk + 18 * nb;
+  a.theta = (const float*)S->theta;
+  a.partials = (float*)S->partials;
+  a.log = (float*)S->log;
+  a.status = S->status;
+  a.iters = S->iters;
+  a.w = (const float*)w;
+  a.disturbance = cf->disturbance;
+  a.write_log = (cf->write_log && S->log) ? 1 : 0;
+  a.seed = cf->seed;
+  for (int f = 0; f < 3; ++f) {
+    a.wlo[f] = float(cf->w_low[f]);
+    a.whi[f] = float(cf->w_high[f]);
+  }
+  const int lanes = S->lanes;
+  const dim3 grid = grid_for(B * lanes);
+#define FAST_CASE(m)                                                                                       \
+  case m:                                                                                                  \
+    if (lanes == 2)                                                                                        \
+      hipLaunchKernelGGL((fk::tube_fast_kernel<m, 2>), grid, dim3(kBlock), 0, st, kk);                   \
+    else                                                                                                   \
+      hipLaunchKernelGGL((fk::tube_fast_kernel<m, 1>), grid, dim3(kBlock), 0, st, kk);                   \
+    break;
+  switch (sp->n_obstacles) {
+#ifdef DTMPC_FAST_M_ONLY
+    FAST_CASE(DTMPC_FAST_M_ONLY)
+#else
+    FAST_CASE(1) FAST_CASE(2) FAST_CASE(3) FAST_CASE(4) FAST_CASE(5) FAST_CASE(6) FAST_CASE(7) FAST_CASE(8)
+#endif
+    default: return set_err(DTMPC_ERR_BAD_ARG, "fast tube step: obstacle count not instantiated");
+  }
+#undef FAST_CASE
+  return check_launch("tube_fast_kernel");
+}
+
+}  // namespace dtmpc

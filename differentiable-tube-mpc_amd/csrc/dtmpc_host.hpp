@@ -168,4 +168,9 @@ inline int check_cost(const dtmpc_cost* c, const void* Xref, const void* Uref) {
 
 inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + kBlock - 1) / kBlock)); }
 
+// the specialised tube step of the paper configuration (dtmpc_fast.hip)
+bool tube_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf);
+int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
+                     const dtmpc_tube_state* S, const void* w, hipStream_t st);
+
 }  // namespace dtmpc

@@ -654,6 +654,7 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
   if (cfg->disturbance == 0 && !w) return set_err(DTMPC_ERR_BAD_ARG, "injected disturbance w is NULL");
   if (cfg->disturbance != 0 && cfg->disturbance != 1) return set_err(DTMPC_ERR_BAD_ARG, "bad disturbance mode");
   hipStream_t st = (hipStream_t)stream;
+  if (tube_fast_eligible(dtype, spec, cfg)) return launch_tube_fast(spec, cfg, B, global_offset, step, S, w, st);
   if (dtype == DTMPC_F32) return launch_tube<float>(spec, cfg, B, global_offset, step, S, w, st);
   if (dtype == DTMPC_F64) return launch_tube<double>(spec, cfg, B, global_offset, step, S, w, st);
   return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
