@@ -20,6 +20,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -64,10 +65,13 @@ def initial_states(lo: int, hi: int, device, dtype) -> torch.Tensor:
 
 
 def pmc_traffic(batch: int):
-    """Per-launch HBM bytes of tube_step_kernel from a committed rocprofv3 --pmc summary (or None).
+    """Per-launch HBM bytes of the tube-step kernel from a committed rocprofv3 --pmc summary (or None).
     FETCH_SIZE is doubled (gfx950 under-reports wide coalesced reads by 2x, MI355X_MICROARCH.md §HBM)."""
+    def newest_first(path):  # profiles/rNN/pmc_vMM.json: the highest round, then the highest version
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.relpath(path, REPO))]
+
     best = None
-    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True)):
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True), key=newest_first):
         try:
             d = json.load(open(p))
         except Exception:

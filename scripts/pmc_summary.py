@@ -2,7 +2,8 @@
 
 usage: python scripts/pmc_summary.py gpurun_out/prof_TAG OUT.json [--batch B]
 
-Per-dispatch means of every counter for tube_step_kernel, plus the HBM bytes per launch:
+Per-dispatch means of every counter for the tube-step kernel (tube_fast_kernel, the specialised paper
+configuration, or the generic tube_step_kernel -- whichever the bench launched), plus the HBM bytes per launch:
   raw = FETCH_SIZE + WRITE_SIZE (KiB -> bytes), and the calibrated figure, where FETCH / WRITE are each
   divided by the ratio measured/known on the known-byte rollout launch of scripts/pmc_calib.py (same
   dword-per-lane access pattern, past the Infinity Cache).  MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE
@@ -15,13 +16,20 @@ import sys
 from collections import defaultdict
 
 
+TUBE_KERNELS = ("tube_fast_kernel", "tube_step_kernel")
+
+
+def _match(name, kern):
+    return any(k in name for k in kern) if isinstance(kern, tuple) else kern in name
+
+
 def counters(root, kern, sub="*"):
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(root, sub, "run_counter_collection.csv")) + \
             glob.glob(os.path.join(root, sub, "*", "run_counter_collection.csv")):
         per = defaultdict(float)
         for r in csv.DictReader(open(f)):
-            if kern not in r["Kernel_Name"]:
+            if not _match(r["Kernel_Name"], kern):
                 continue
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
         for (d, c), v in per.items():
@@ -32,8 +40,8 @@ def counters(root, kern, sub="*"):
 def kernel_stats(root, kern):
     for f in glob.glob(os.path.join(root, "trace", "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if kern in r["Name"]:
-                return {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+            if _match(r["Name"], kern):
+                return {"name": r["Name"][:120], "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
                         "max_ns": float(r["MaxNs"])}
     return None
 
@@ -41,14 +49,15 @@ def kernel_stats(root, kern):
 def main():
     root, out = sys.argv[1], sys.argv[2]
     batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 65536
-    tube = {k: v for sub in ("fetch", "write", "sq1", "sq2", "tcc") for k, v in counters(root, "tube_step_kernel", sub).items()}
+    tube = {k: v for sub in ("fetch", "write", "sq1", "sq2", "tcc") for k, v in counters(root, TUBE_KERNELS, sub).items()}
     cal_f = counters(root, "rollout_kernel", "cal_fetch")
     cal_w = counters(root, "rollout_kernel", "cal_write")
     N = 50
     Bc = 262144
     known_r, known_w = 4 * Bc * (4 + 2 * N), 4 * Bc * 4 * (N + 1)
-    res = {"kernel": "tube_step_kernel<float, 6> (7 alphas: 6 rolled out + alpha = 0 from the current tape)", "batch": batch, "counters_per_dispatch": tube,
-           "kernel_trace": kernel_stats(root, "tube_step_kernel")}
+    ks = kernel_stats(root, TUBE_KERNELS)
+    res = {"kernel": (ks or {}).get("name", "tube step") + " (7 alphas: 6 rolled out + alpha = 0 from the current tape)",
+           "batch": batch, "counters_per_dispatch": tube, "kernel_trace": ks}
     if "FETCH_SIZE" in tube and "WRITE_SIZE" in tube:
         raw = 1024.0 * (tube["FETCH_SIZE"] + tube["WRITE_SIZE"])
         res["tube_step_bytes_raw"] = raw
