@@ -6,7 +6,9 @@ path), csrc/dtmpc_receding.hip (receding-horizon nominal MPC driver).
 """
 from __future__ import annotations
 
+import hashlib
 import os
+import shutil
 import subprocess
 import sys
 
@@ -18,6 +20,7 @@ DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solve
     os.path.join(os.path.dirname(HERE), "include", "dtmpc.h")
 ]
 OUT = os.path.join(HERE, "diff_tube_mpc_strict_pt", "libdtmpc.so")
+CACHE = os.path.join(HERE, "build", "obj")  # object cache keyed by the command line + source texts
 ARCH = os.environ.get("DTMPC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
@@ -30,29 +33,45 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in [*SRCS, *DEPS, __file__])
 
 
-def build(force: bool = False, variant: str = "", defines=()) -> str:
+def _key(cmd, src) -> str:
+    h = hashlib.sha256(" ".join(cmd).encode())
+    for p in [src, *DEPS]:
+        h.update(open(p, "rb").read())
+    return h.hexdigest()[:24]
+
+
+def build(force: bool = False, variant: str = "", defines=(), only=()) -> str:
     """Build the library.  ``variant`` (with extra ``-D`` defines) writes libdtmpc_<variant>.so next to
     the product library, for A/B kernel experiments loaded through DTMPC_LIBRARY; it never replaces
-    libdtmpc.so."""
+    libdtmpc.so.  ``only`` restricts the defines / extra flags to the named translation units (e.g.
+    ``dtmpc_fast``); objects are cached under build/obj by command line and source text, so a variant
+    recompiles only the units its flags reach."""
     out = OUT if not variant else OUT.replace("libdtmpc.so", f"libdtmpc_{variant}.so")
     if not variant and not force and up_to_date():
         return out
+    os.makedirs(CACHE, exist_ok=True)
     objs = []
     procs = []
     for src in SRCS:
-        obj = out + "." + os.path.splitext(os.path.basename(src))[0] + ".o"
-        extra = os.environ.get("DTMPC_EXTRA_FLAGS", "").split() if variant else []
-        cmd = [HIPCC, *FLAGS, *extra, *[f"-D{d}" for d in defines], "-c", "-o", obj, src]
-        print("[build]", " ".join(cmd), flush=True)
-        procs.append(subprocess.Popen(cmd))
+        tu = os.path.splitext(os.path.basename(src))[0]
+        reach = not only or tu in only
+        extra = os.environ.get("DTMPC_EXTRA_FLAGS", "").split() if variant and reach else []
+        defs = [f"-D{d}" for d in defines] if reach else []
+        cmd = [HIPCC, *FLAGS, *extra, *defs, "-c"]
+        obj = os.path.join(CACHE, f"{tu}.{_key(cmd, src)}.o")
         objs.append(obj)
-    if any([p.wait() != 0 for p in procs]):
+        if os.path.exists(obj):  # content-keyed: safe to reuse even under --force
+            continue
+        full = [*cmd, "-o", obj + ".tmp", src]
+        print("[build]", " ".join(full), flush=True)
+        procs.append((subprocess.Popen(full), obj))
+    if any([p.wait() != 0 for p, _ in procs]):
         raise subprocess.CalledProcessError(1, "hipcc")
+    for _, obj in procs:
+        os.replace(obj + ".tmp", obj)
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    for o in objs:
-        os.remove(o)
     os.replace(out + ".tmp", out)
     return out
 
@@ -64,5 +83,6 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--variant", default="")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--only", action="append", default=[], help="translation unit(s) the -D / extra flags reach")
     a = ap.parse_args()
-    print(build(force=a.force, variant=a.variant, defines=a.defines))
+    print(build(force=a.force, variant=a.variant, defines=a.defines, only=tuple(a.only)))

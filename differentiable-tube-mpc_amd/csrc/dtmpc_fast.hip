@@ -158,8 +158,13 @@ template <> struct VT<f2> { static constexpr int W = 2; };
 
 __device__ __forceinline__ float vmin(float a, float b) { return m_min(a, b); }
 __device__ __forceinline__ f2 vmin(f2 a, f2 b) { return f2{m_min(a.x, b.x), m_min(a.y, b.y)}; }
-__device__ __forceinline__ float vclamp(float v, float lo, float hi) { return clampv(v, lo, hi); }
-__device__ __forceinline__ f2 vclamp(f2 v, float lo, float hi) { return f2{clampv(v.x, lo, hi), clampv(v.y, lo, hi)}; }
+// torch.clamp (core/control.py:61-64) as v_maximum3_f32 / v_minimum3_f32: IEEE 754-2019 maximum /
+// minimum propagate NaN like the compare-select form, without a VCC write (no hazard wait states)
+__device__ __forceinline__ float vclamp(float v, float lo, float hi) {
+  return __builtin_elementwise_minimum(__builtin_elementwise_maximum(v, lo), hi);
+}
+__device__ __forceinline__ f2 vclamp(f2 v, float lo, float hi) { return f2{vclamp(v.x, lo, hi), vclamp(v.y, lo, hi)}; }
+__device__ __forceinline__ float vmaxnan(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 __device__ __forceinline__ float vexp(float x) { return m_exp(x); }
 __device__ __forceinline__ f2 vexp(f2 x) { return pk_exp(x); }
 __device__ __forceinline__ float vlog(float x) { return m_log(x); }
@@ -177,15 +182,16 @@ __device__ __forceinline__ float bar_relaxed(const FP& p, float z) {
   const float diff = z - p.a;
   return (p.inv_a - diff / p.a2) + (diff * diff) / p.a3;
 }
+// 1 / max(z, eps) with max NaN-propagating (= the reference's torch.clamp_min then reciprocal)
 __device__ __forceinline__ float vbarrier(const FP& p, float z) {
   DTMPC_NOCONTRACT
-  float r = m_rcp(z < p.eps ? p.eps : z);
+  float r = m_rcp(vmaxnan(z, p.eps));
   if (!(z >= p.a)) r = bar_relaxed(p, z);
   return r;
 }
 __device__ __forceinline__ f2 vbarrier(const FP& p, f2 z) {
   DTMPC_NOCONTRACT
-  f2 r = f2{m_rcp(z.x < p.eps ? p.eps : z.x), m_rcp(z.y < p.eps ? p.eps : z.y)};
+  f2 r = f2{m_rcp(vmaxnan(z.x, p.eps)), m_rcp(vmaxnan(z.y, p.eps))};
   if (!(z.x >= p.a) || !(z.y >= p.a)) {
     if (!(z.x >= p.a)) r.x = bar_relaxed(p, z.x);
     if (!(z.y >= p.a)) r.y = bar_relaxed(p, z.y);
@@ -383,7 +389,7 @@ __device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const fl
         nq1 = S.Ur.ld(k + 1, 1);
       }
     }
-    const float u0 = clampv(v0, p.umin0, p.umax0), u1 = clampv(v1, p.umin1, p.umax1);
+    const float u0 = vclamp(v0, p.umin0, p.umax0), u1 = vclamp(v1, p.umin1, p.umax1);
     S.U.st(k, 0, u0);
     S.U.st(k, 1, u1);
     if (want_cost) J = J + stage<TRACK>(c, s0, s1, s2, sb, u0, u1, r0, r1, r2, q0, q1);
@@ -518,57 +524,177 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
 }
 
 // ---------------------------------------------------------------------------------------------
-// line search (core/ddp.py:256-301) over this lane's candidates: NP packed pairs + NS singles
-// (P = 1: the six candidates as three pairs; P = 2: three per lane, one pair + one single), then the
-// first strict minimum over the ORIGINAL candidate order, combined over the lane pair when P = 2,
-// and the alpha = 0 rule (it is the current tape, cost Jprev).  Returns the chosen original position
-// (or -1 if any candidate or Jprev is non-finite), its cost and alpha.
+// line search (core/ddp.py:256-301) over this lane's NL candidates, held as NPR two-wide pairs (an odd
+// NL repeats its last candidate in the second slot of the last pair: a packed op costs one issue slot
+// for one element or two).  One step of the rollout is written operation by operation ACROSS the
+// pairs, so the instruction stream interleaves NPR independent chains: no dependent pair of packed
+// ops / compare-select sits back to back (each such pair costs an s_nop wait state on gfx950).
+// Arithmetic per candidate is the scalar forward pass (fhat, stage) operation for operation.
+template <int NPR>
+struct Cand {
+  f2 a0[NPR], a1[NPR], a2[NPR], ab[NPR], Bp[NPR], J[NPR], al[NPR];
+};
+
+// sin / cos of NPR pairs (pk_sincos per pair); one range test for all of them
+template <int NPR>
+__device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
+  float m = __builtin_fabsf(x[0].x);
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(x[q].x), __builtin_fabsf(x[q].y)));
+#ifndef DTMPC_OCML_SINCOS
+  if (__builtin_expect(m <= 65536.0f, 1)) {
+    f2 qq[NPR], r[NPR], z[NPR], s[NPR], c[NPR];
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) qq[q] = f2{__builtin_rintf(x[q].x * k2oPi), __builtin_rintf(x[q].y * k2oPi)};
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) r[q] = __builtin_elementwise_fma(-qq[q], f2(kPio2A), x[q]);
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) r[q] = __builtin_elementwise_fma(-qq[q], f2(kPio2B), r[q]);
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) r[q] = __builtin_elementwise_fma(-qq[q], f2(kPio2C), r[q]);
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) z[q] = r[q] * r[q];
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      f2 ps = __builtin_elementwise_fma(z[q], f2(kSinS3), f2(kSinS2));
+      f2 pc = __builtin_elementwise_fma(z[q], f2(kCosK3), f2(kCosK2));
+      ps = __builtin_elementwise_fma(z[q], ps, f2(kSinS1));
+      pc = __builtin_elementwise_fma(z[q], pc, f2(kCosK1));
+      s[q] = __builtin_elementwise_fma(r[q] * z[q], ps, r[q]);
+      c[q] = __builtin_elementwise_fma(z[q] * z[q], pc, __builtin_elementwise_fma(f2(-0.5f), z[q], f2(1.0f)));
+    }
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      const int j0 = (int)qq[q].x & 3, j1 = (int)qq[q].y & 3;
+      const float so0 = (j0 & 1) ? c[q].x : s[q].x, co0 = (j0 & 1) ? s[q].x : c[q].x;
+      const float so1 = (j1 & 1) ? c[q].y : s[q].y, co1 = (j1 & 1) ? s[q].y : c[q].y;
+      sn[q] = f2{(j0 & 2) ? -so0 : so0, (j1 & 2) ? -so1 : so1};
+      cs[q] = f2{((j0 + 1) & 2) ? -co0 : co0, ((j1 + 1) & 2) ? -co1 : co1};
+    }
+    return;
+  }
+#endif
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    float s0, c0, s1, c1;
+    m_sincos(x[q].x, &s0, &c0);
+    m_sincos(x[q].y, &s1, &c1);
+    sn[q] = f2{s0, s1};
+    cs[q] = f2{c0, c1};
+  }
+}
+
+// one step of the NPR pairs' rollouts: feedback + clamp, stage cost, DBaS-augmented Dubins move
+template <bool TRACK, int M, int NPR>
+__device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepIn& s, Cand<NPR>& C) {
+  DTMPC_NOCONTRACT
+  f2 u0[NPR], u1[NPR];
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    const f2 e0 = C.a0[q] - s.X0, e1 = C.a1[q] - s.X1, e2 = C.a2[q] - s.X2, e3 = C.ab[q] - s.X3;
+    const f2 du0 = s.kk.x + (s.Ka.x * e0 + s.Ka.y * e1 + s.Ka.z * e2 + s.Ka.w * e3);
+    const f2 du1 = s.kk.y + (s.Kb.x * e0 + s.Kb.y * e1 + s.Kb.z * e2 + s.Kb.w * e3);
+    u0[q] = s.V0 + C.al[q] * du0;
+    u1[q] = s.V1 + C.al[q] * du1;
+  }
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    u0[q] = vclamp(u0[q], p.umin0, p.umax0);
+    u1[q] = vclamp(u1[q], p.umin1, p.umax1);
+  }
+#pragma unroll
+  for (int q = 0; q < NPR; ++q)
+    C.J[q] = C.J[q] + stage<TRACK>(c, C.a0[q], C.a1[q], C.a2[q], C.ab[q], u0[q], u1[q], s.r0, s.r1, s.r2, s.q0, s.q1);
+  f2 sn[NPR], cs[NPR];
+  sincos_pairs<NPR>(C.a2, sn, cs);
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    const f2 dv = p.dt * u0[q];
+    C.a0[q] = C.a0[q] + dv * cs[q];
+    C.a1[q] = C.a1[q] + dv * sn[q];
+    C.a2[q] = C.a2[q] + p.dt * u1[q];
+  }
+  // smooth-min h over the M obstacles (h_sm), all pairs together
+  f2 hi[M][NPR], hm[NPR];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      const f2 dx = C.a0[q] - p.cx[i];
+      const f2 dy = C.a1[q] - p.cy[i];
+      hi[i][q] = dx * dx + dy * dy - p.r2[i];
+      hm[q] = i == 0 ? hi[0][q] : vmin(hm[q], hi[i][q]);
+    }
+  f2 zmax[NPR], se[NPR], z[NPR];
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) zmax[q] = p.neg_beta * hm[q];
+#pragma unroll
+  for (int i = 0; i < M; ++i)
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      const f2 e = vexp(p.neg_beta * hi[i][q] - zmax[q]);
+      se[q] = i == 0 ? e : se[q] + e;  // = 0 + e_0 + ...: e_0 >= 0, so 0 + e_0 == e_0 bitwise
+    }
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) z[q] = p.neg_inv_beta * (zmax[q] + vlog(se[q]));
+  // relaxed inverse barrier: the reciprocal for every element, the quadratic branch (z < a) once
+  // per step for whichever elements need it
+  f2 Bn[NPR];
+  float zmin = z[0].x;
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    Bn[q] = f2{m_rcp(vmaxnan(z[q].x, p.eps)), m_rcp(vmaxnan(z[q].y, p.eps))};
+    zmin = __builtin_fminf(zmin, __builtin_fminf(z[q].x, z[q].y));
+  }
+  if (!(zmin >= p.a)) {
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      if (!(z[q].x >= p.a)) Bn[q].x = bar_relaxed(p, z[q].x);
+      if (!(z[q].y >= p.a)) Bn[q].y = bar_relaxed(p, z[q].y);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    C.ab[q] = Bn[q] - p.gamma * (C.Bp[q] - C.ab[q]);
+    C.Bp[q] = Bn[q];
+  }
+}
+
+// Returns the chosen original position (or -1 if any candidate or Jprev is non-finite), its cost
+// and alpha.  P = 1: the six candidates as three pairs; P = 2: three per lane (two pairs, the last
+// one doubled), the pair of lanes combining their minima by one DPP swap.
 template <bool TRACK, int M, int P>
 __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FIlqr& cf, const float* x0, float Bc0,
                                            const Solve<TRACK>& S, float Jprev, int h, float& bestJ, float& al_out) {
   DTMPC_NOCONTRACT
-  constexpr int NL = NC / P;       // candidates of this lane
-  constexpr int NP = NL / 2, NS = NL % 2;
+  constexpr int NL = NC / P;          // candidates of this lane
+  constexpr int NPR = (NL + 1) / 2;   // pairs
   const int N = p.N;
-  const int c0 = h * NL;           // this lane's first candidate (index into cf.cal / cf.cpos)
-  f2 a0[NP > 0 ? NP : 1], a1[NP > 0 ? NP : 1], a2[NP > 0 ? NP : 1], ab[NP > 0 ? NP : 1], Bp[NP > 0 ? NP : 1],
-      Jp[NP > 0 ? NP : 1], alp[NP > 0 ? NP : 1];
-  float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bs = Bc0, Js = 0.f, als = 0.f;
+  const int c0 = h * NL;              // this lane's first candidate (index into cf.cal / cf.cpos)
+  Cand<NPR> C;
 #pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    a0[q] = x0[0];
-    a1[q] = x0[1];
-    a2[q] = x0[2];
-    ab[q] = x0[3];
-    Bp[q] = Bc0;
-    Jp[q] = 0.f;
-    alp[q] = P == 1 ? f2{cf.cal[2 * q], cf.cal[2 * q + 1]}
-                    : (h ? f2{cf.cal[NL + 2 * q], cf.cal[NL + 2 * q + 1]} : f2{cf.cal[2 * q], cf.cal[2 * q + 1]});
+  for (int q = 0; q < NPR; ++q) {
+    C.a0[q] = x0[0];
+    C.a1[q] = x0[1];
+    C.a2[q] = x0[2];
+    C.ab[q] = x0[3];
+    C.Bp[q] = Bc0;
+    C.J[q] = 0.f;
+    const int i0 = 2 * q, i1 = 2 * q + 1 < NL ? 2 * q + 1 : NL - 1;
+    C.al[q] = P == 1 ? f2{cf.cal[i0], cf.cal[i1]} : (h ? f2{cf.cal[NL + i0], cf.cal[NL + i1]} : f2{cf.cal[i0], cf.cal[i1]});
   }
-  if (NS) als = h ? cf.cal[NL + NL - 1] : cf.cal[NL - 1];
-  StepIn cur, nxt;
-  load_step<TRACK>(nxt, S, 0);
-  for (int k = 0; k < N; ++k) {
-    cur = nxt;
-    if (k + 1 < N) load_step<TRACK>(nxt, S, k + 1);
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-      const f2 e0 = a0[q] - cur.X0, e1 = a1[q] - cur.X1, e2 = a2[q] - cur.X2, e3 = ab[q] - cur.X3;
-      const f2 du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
-      const f2 du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
-      const f2 u0 = vclamp(cur.V0 + alp[q] * du0, p.umin0, p.umax0);
-      const f2 u1 = vclamp(cur.V1 + alp[q] * du1, p.umin1, p.umax1);
-      Jp[q] = Jp[q] + stage<TRACK>(c, a0[q], a1[q], a2[q], ab[q], u0, u1, cur.r0, cur.r1, cur.r2, cur.q0, cur.q1);
-      fhat<M>(p, a0[q], a1[q], a2[q], ab[q], u0, u1, Bp[q]);
-    }
-    if (NS) {
-      const float e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
-      const float du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
-      const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
-      const float u0 = clampv(cur.V0 + als * du0, p.umin0, p.umax0);
-      const float u1 = clampv(cur.V1 + als * du1, p.umin1, p.umax1);
-      Js = Js + stage<TRACK>(c, s0, s1, s2, sb, u0, u1, cur.r0, cur.r1, cur.r2, cur.q0, cur.q1);
-      fhat<M>(p, s0, s1, s2, sb, u0, u1, Bs);
+  // two step buffers in turn (no copies), each refilled two steps ahead; the refill index is clamped
+  // (a redundant load of the last row instead of a branch)
+  StepIn A, Bs;
+  const int N1 = N - 1;
+  load_step<TRACK>(A, S, 0);
+  load_step<TRACK>(Bs, S, N1 < 1 ? N1 : 1);
+  for (int k = 0; k < N; k += 2) {
+    ls_step<TRACK, M, NPR>(p, c, A, C);
+    load_step<TRACK>(A, S, k + 2 < N1 ? k + 2 : N1);
+    if (k + 1 < N) {
+      ls_step<TRACK, M, NPR>(p, c, Bs, C);
+      load_step<TRACK>(Bs, S, k + 3 < N1 ? k + 3 : N1);
     }
   }
   float r0 = 0.f, r1 = 0.f, r2 = 0.f;
@@ -577,18 +703,14 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
     r1 = S.Xr.ld(N, 1);
     r2 = S.Xr.ld(N, 2);
   }
-  float Jc[NL];
+  float Jc[2 * NPR];
   bool ok = true;
 #pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    const f2 Jt = Jp[q] + term<TRACK>(c, a0[q], a1[q], a2[q], ab[q], r0, r1, r2);
+  for (int q = 0; q < NPR; ++q) {
+    const f2 Jt = C.J[q] + term<TRACK>(c, C.a0[q], C.a1[q], C.a2[q], C.ab[q], r0, r1, r2);
     Jc[2 * q] = Jt.x;
     Jc[2 * q + 1] = Jt.y;
     ok = ok && vfinite(Jt);
-  }
-  if (NS) {
-    Jc[NL - 1] = Js + term<TRACK>(c, s0, s1, s2, sb, r0, r1, r2);
-    ok = ok && finite(Jc[NL - 1]);
   }
   // this lane's first strict minimum (its candidates are in increasing original order)
   float bJ = Jc[0];
@@ -672,8 +794,8 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
     const float e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
     const float du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
     const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
-    const float u0 = clampv(cur.V0 + al * du0, p.umin0, p.umax0);
-    const float u1 = clampv(cur.V1 + al * du1, p.umin1, p.umax1);
+    const float u0 = vclamp(cur.V0 + al * du0, p.umin0, p.umax0);
+    const float u1 = vclamp(cur.V1 + al * du1, p.umin1, p.umax1);
     S.U.st(k, 0, u0);
     S.U.st(k, 1, u1);
     fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
@@ -687,19 +809,24 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
 // iLQR for one trajectory (ilqr_traj, core/ddp.py:102-307)
 template <bool TRACK, int M, int P>
 __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const float* x0,
-                                    const Solve<TRACK>& S, int h, int& iters) {
+                                    const Solve<TRACK>& S, int h, int& iters, Prof& pf) {
+  constexpr int ph = TRACK ? 4 : 0;  // phase-timer slots (profiling builds)
   float Jcur = init_tape<TRACK, M>(p, c, x0, S, cf.zpos >= 0 && cf.max_iter > 0);
   const float Bc0 = barrier_at<M>(p, x0[0], x0[1]);
   bool have_prev = false;
   float prev = 0.f;
   iters = 0;
+  pf.mark(ph);
   for (int it = 0; it < cf.max_iter; ++it) {
     iters = it + 1;
     if (!backward<TRACK, M>(p, c, cf.reg, S)) return DTMPC_ST_NONFINITE;
+    pf.mark(ph + 1);
     float bestJ, al;
     const int best = line_search<TRACK, M, P>(p, c, cf, x0, Bc0, S, Jcur, h, bestJ, al);
+    pf.mark(ph + 2);
     if (best < 0) return DTMPC_ST_NONFINITE;
     if (al != 0.f) commit<TRACK, M>(p, al, x0, Bc0, S);
+    pf.mark(ph + 3);
     Jcur = bestJ;
     if (have_prev && m_abs(prev - bestJ) < cf.tol) break;
     have_prev = true;
@@ -892,6 +1019,8 @@ tube_fast_kernel(FK kk) {
   const int gl = blockIdx.x * kBlock + threadIdx.x;
   const int i = P == 1 ? gl : (gl >> 1), h = P == 1 ? 0 : (gl & 1);
   float acc[DTMPC_TUBE_SUMS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  Prof pf;
+  pf.start();
   if (i < B) {
     const size_t nb = (size_t)B;
     const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
@@ -922,7 +1051,7 @@ tube_fast_kernel(FK kk) {
       const FCost cn = K->cn;
       const FIlqr cfn = K->cfn;
       const float xn0[4] = {y0, y1, y2, yb};
-      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, itn);
+      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, itn, pf);
     }
     FCost ca;  // ancillary weights theta (shared by the batch), terminal weight Qa (:885, :891)
     {
@@ -947,8 +1076,9 @@ tube_fast_kernel(FK kk) {
       const FP p = phase_p<M>();
       const FIlqr cfa = K->cfa;
       const float xa0[4] = {x0, x1, x2, xb};
-      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, ita);
+      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, ita, pf);
     }
+    pf.mark(8);
     {  // upper loss, DOC sensitivity and gradient (:915-976)
       KArg* K = kargs();
       const Rec<8> AB8{(char*)K->a.ab8, bb * 8u, lo * 8u};
@@ -956,6 +1086,7 @@ tube_fast_kernel(FK kk) {
       const FP p = phase_p<M>();
       st |= sensitivity<M>(p, ca, Sa, AB8, AB2, acc);
     }
+    pf.mark(9);
     {  // plant step with disturbance, nominal propagation (:990-1001), log, warm-start shift
       KArg* K = kargs();
       const FArgs& a = K->a;
@@ -1029,7 +1160,9 @@ tube_fast_kernel(FK kk) {
         }
       }
     }
+    pf.mark(10);
   }
+  pf.flush();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) {
@@ -1165,3 +1298,16 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
 }
 
 }  // namespace dtmpc
+
+#ifdef DTMPC_PROFILE
+extern "C" {
+// profiling builds only (not part of include/dtmpc.h): this translation unit's phase-cycle accumulators
+int dtmpc_prof_read_fast(void* host16) {
+  return hipMemcpyFromSymbol(host16, HIP_SYMBOL(dtmpc::g_prof), 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+int dtmpc_prof_reset_fast(void) {
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(dtmpc::g_prof), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+}
+#endif

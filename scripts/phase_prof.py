@@ -22,21 +22,24 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=65536)
 a = ap.parse_args()
 lib = _lib.load()
-lib.dtmpc_prof_read.argtypes = [C.c_void_p]
+fast = os.environ.get("DTMPC_FAST", "1") != "0"  # the specialised kernel has its own accumulators
+rd = lib.dtmpc_prof_read_fast if fast else lib.dtmpc_prof_read
+rs = lib.dtmpc_prof_reset_fast if fast else lib.dtmpc_prof_reset
+rd.argtypes = [C.c_void_p]
 st = bench_setup("f32")
 mpc = TubeMPC(st, batch=a.batch, device="cuda", dtype=torch.float32, disturbance="philox", seed=0)
 x0 = initial_states(0, a.batch, "cuda", torch.float32)
 mpc.reset(x0)
 mpc.step()
 torch.cuda.synchronize()
-lib.dtmpc_prof_reset()
+rs()
 mpc.reset(x0)
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 mpc.step(kernel_events=(e0, e1))
 torch.cuda.synchronize()
 buf = np.zeros(16, np.uint64)
-assert lib.dtmpc_prof_read(buf.ctypes.data) == 0
-waves = a.batch // 64
+assert rd(buf.ctypes.data) == 0
+waves = a.batch * mpc.lanes // 64 if hasattr(mpc, "lanes") else a.batch // 64
 cyc = buf[:11].astype(np.float64) / waves
 tot = cyc.sum()
 print(f"kernel {e0.elapsed_time(e1):.3f} ms; per-wave total {tot:.4g} cycles")
