@@ -96,6 +96,10 @@ __device__ __forceinline__ float* gaddr(const char* base, size_t row_off, unsign
   return (float*)(row + lane_off);
 }
 
+// a step index known to be wave-uniform (readfirstlane: free when the compiler already keeps it in an
+// SGPR; it pins a clamped refill index to the scalar unit, where gaddr needs its row base)
+__device__ __forceinline__ int uidx(int k) { return __builtin_amdgcn_readfirstlane(k); }
+
 // per-lane byte offsets of field f of a SoA row: trajectory * 4 + f * B * 4 (four VGPRs shared by
 // every SoA tape of the batch)
 struct Lane {
@@ -691,10 +695,10 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   load_step<TRACK>(Bs, S, N1 < 1 ? N1 : 1);
   for (int k = 0; k < N; k += 2) {
     ls_step<TRACK, M, NPR>(p, c, A, C);
-    load_step<TRACK>(A, S, k + 2 < N1 ? k + 2 : N1);
+    load_step<TRACK>(A, S, uidx(k + 2 < N1 ? k + 2 : N1));
     if (k + 1 < N) {
       ls_step<TRACK, M, NPR>(p, c, Bs, C);
-      load_step<TRACK>(Bs, S, k + 3 < N1 ? k + 3 : N1);
+      load_step<TRACK>(Bs, S, uidx(k + 3 < N1 ? k + 3 : N1));
     }
   }
   float r0 = 0.f, r1 = 0.f, r2 = 0.f;
@@ -806,6 +810,30 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
   }
 }
 
+#ifdef DTMPC_PROFILE
+// profiling builds: line-search outcome statistics per solve (TRACK = 0 nominal, 1 ancillary), 32 slots
+// each: [0..7] winners by original alpha position (lanes), [8] wave-iterations, [9] waves where every
+// lane keeps its tape (alpha = 0), [10] every lane takes the first alpha, [11] every lane one of the two
+__device__ unsigned long long g_lsstat[64];
+__device__ __forceinline__ void ls_stat(int trk, int best, float al, const FIlqr& cf) {
+  unsigned long long* g = g_lsstat + 32 * trk;
+  const bool lead = (threadIdx.x & 63) == (__builtin_ctzll(__ballot(1)));
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const unsigned long long b = __ballot(best == q);
+    if (lead && b) atomicAdd(g + q, (unsigned long long)__builtin_popcountll(b));
+  }
+  const bool z = al == 0.f, f = al == cf.cal[0] && best == cf.cpos[0];
+  const unsigned long long act = __ballot(1);
+  if (lead) {
+    atomicAdd(g + 8, 1ull);
+    if (__ballot(z) == act) atomicAdd(g + 9, 1ull);
+    if (__ballot(f) == act) atomicAdd(g + 10, 1ull);
+    if (__ballot(z || f) == act) atomicAdd(g + 11, 1ull);
+  }
+}
+#endif
+
 // iLQR for one trajectory (ilqr_traj, core/ddp.py:102-307)
 template <bool TRACK, int M, int P>
 __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const float* x0,
@@ -824,6 +852,9 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
     float bestJ, al;
     const int best = line_search<TRACK, M, P>(p, c, cf, x0, Bc0, S, Jcur, h, bestJ, al);
     pf.mark(ph + 2);
+#ifdef DTMPC_PROFILE
+    ls_stat(TRACK ? 1 : 0, best, al, cf);
+#endif
     if (best < 0) return DTMPC_ST_NONFINITE;
     if (al != 0.f) commit<TRACK, M>(p, al, x0, Bc0, S);
     pf.mark(ph + 3);
@@ -1306,8 +1337,12 @@ int dtmpc_prof_read_fast(void* host16) {
   return hipMemcpyFromSymbol(host16, HIP_SYMBOL(dtmpc::g_prof), 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
 }
 int dtmpc_prof_reset_fast(void) {
-  unsigned long long z[16] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(dtmpc::g_prof), z, sizeof(z)) == hipSuccess ? 0 : 1;
+  unsigned long long z[64] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(dtmpc::fk::g_lsstat), z, sizeof(z)) != hipSuccess) return 1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(dtmpc::g_prof), z, 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+int dtmpc_prof_lsstat_fast(void* host64) {
+  return hipMemcpyFromSymbol(host64, HIP_SYMBOL(dtmpc::fk::g_lsstat), 64 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
 }
 }
 #endif

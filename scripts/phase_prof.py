@@ -47,3 +47,14 @@ for n, c in zip(NAMES, cyc):
     print(f"{n:16s} {c:12.4g} cyc/wave {100 * c / tot:6.1f} %")
 print("per step-pass (N=50): nom.backward/it %.0f, nom.ls/it %.0f, nom.commit/it %.0f cycles" %
       (cyc[1] / 10 / 50, cyc[2] / 10 / 50, cyc[3] / 10 / 50))
+
+if fast and hasattr(lib, "dtmpc_prof_lsstat_fast"):
+    st = np.zeros(64, np.uint64)
+    lib.dtmpc_prof_lsstat_fast.argtypes = [C.c_void_p]
+    assert lib.dtmpc_prof_lsstat_fast(st.ctypes.data) == 0
+    for name, o in (("nominal", 0), ("ancillary", 32)):
+        w = st[o:o + 8].astype(np.float64)
+        n = max(float(st[o + 8]), 1.0)
+        print(f"{name}: winners by alpha position {[int(x) for x in w]} (share {np.round(w / max(w.sum(), 1), 3).tolist()}); "
+              f"wave-iterations {int(st[o + 8])}: all keep {st[o + 9] / n:.3f}, all first {st[o + 10] / n:.3f}, "
+              f"all keep-or-first {st[o + 11] / n:.3f}")
