@@ -55,7 +55,8 @@ struct FIlqr {
 };
 
 struct FArgs {
-  int B;
+  int B;       // trajectories of the batch: the stride of the ABI SoA arrays
+  int i0, Bc;  // this launch's chunk of trajectories [i0, i0 + Bc): the workspace records hold Bc
   long long goff, step;
   float* x;
   float* b;
@@ -65,10 +66,9 @@ struct FArgs {
   float* Unom;
   float* Xaux;
   float* Uaux;
-  float* gK;   // [N][B][8] iLQR / sensitivity gains K
-  float* gk;   // [N][B][2] k
-  float* ab8;  // [N][B][8] sensitivity: a02 a12 a30 a31 a32 b00 b10 b30
-  float* ab2;  // [N][B][2] b31, active set
+  float* work;  // workspace: the per-lane records below, one buffer resource (< 2^31 bytes)
+  unsigned wsz;  // bytes of it the records use
+  unsigned oXn, oUn, oXa, oUa, oK, ok, oA8, oA2;  // byte offsets of the record arrays in the workspace
   const float* theta;
   float* partials;
   float* log;
@@ -136,14 +136,60 @@ __device__ __forceinline__ f2 ld2(const float* q) { return *(const f2*)__builtin
 __device__ __forceinline__ void st4(float* q, f4 v) { *(f4*)__builtin_assume_aligned(q, 16) = v; }
 __device__ __forceinline__ void st2(float* q, f2 v) { *(f2*)__builtin_assume_aligned(q, 8) = v; }
 
+// ---------------------------------------------------------------------------------------------
+// the workspace records.  Every per-step array the solver iterates on lives in the workspace as
+// per-lane records [rows][Bc][W] (AoS: one trajectory's row is W contiguous floats), addressed through
+// ONE buffer resource: element (row k, field f) of this lane is at soffset = base + k * rs (SGPR, a
+// running scalar add per step) + voffset = lane * W * 4 (a VGPR fixed for the kernel) + the field's
+// byte offset.  A row of a record is one 16-byte (or 8-byte) access, and every array is dense (no
+// padding: a padded record costs its padding in HBM reads -- measured +25 % traffic with 32-byte XU
+// and 48-byte gain records).
+//   X   [N+1][Bc][4]  x0 x1 x2 b        U  [N][Bc][2]  u0 u1      (nominal and ancillary tapes)
+//   K   [N][Bc][8]    K00..K03 K10..K13 k  [N][Bc][2]  k0 k1      (gains)
+//   A8  [N][Bc][8]    a02 a12 a30 a31 a32 b00 b10 b30   A2 [N][Bc][2] b31 act  (sensitivity scratch)
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+
+struct RA {
+  unsigned base, rs, lo;  // uniform base and row stride (bytes), per-lane offset (bytes)
+  __device__ __forceinline__ unsigned so(int k) const { return base + (unsigned)k * rs; }
+};
+#ifndef DTMPC_FAST_GLOBAL
+__device__ __forceinline__ f4 rld4(Rsrc r, const RA& a, int k, unsigned off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off, a.so(k), 0));
+}
+__device__ __forceinline__ f2 rld2(Rsrc r, const RA& a, int k, unsigned off) {
+  return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, a.lo + off, a.so(k), 0));
+}
+__device__ __forceinline__ void rst4(Rsrc r, const RA& a, int k, unsigned off, f4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, a.lo + off, a.so(k), 0);
+}
+__device__ __forceinline__ void rst2(Rsrc r, const RA& a, int k, unsigned off, f2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, a.lo + off, a.so(k), 0);
+}
+#else  // A/B: the same records through global loads / stores with a scalar row base
+__device__ __forceinline__ const char* kargs_ws();
+__device__ __forceinline__ f4 rld4(Rsrc, const RA& a, int k, unsigned off) {
+  return *(const f4*)gaddr(kargs_ws(), (size_t)a.so(k), a.lo + off);
+}
+__device__ __forceinline__ f2 rld2(Rsrc, const RA& a, int k, unsigned off) {
+  return *(const f2*)gaddr(kargs_ws(), (size_t)a.so(k), a.lo + off);
+}
+__device__ __forceinline__ void rst4(Rsrc, const RA& a, int k, unsigned off, f4 v) {
+  *(f4*)gaddr(kargs_ws(), (size_t)a.so(k), a.lo + off) = v;
+}
+__device__ __forceinline__ void rst2(Rsrc, const RA& a, int k, unsigned off, f2 v) {
+  *(f2*)gaddr(kargs_ws(), (size_t)a.so(k), a.lo + off) = v;
+}
+#endif
+
 struct Gains {
-  Rec<8> K;
-  Rec<2> k;
-  __device__ __forceinline__ void store(int s, const float* Kk, const float* kk) const {
-    float* q = K.p(s);
-    st4(q, f4{Kk[0], Kk[1], Kk[2], Kk[3]});
-    st4(q + 4, f4{Kk[4], Kk[5], Kk[6], Kk[7]});
-    st2(k.p(s), f2{kk[0], kk[1]});
+  RA K, k;  // K and k records
+  __device__ __forceinline__ void store(Rsrc r, int s, const float* Kk, const float* kk) const {
+    rst4(r, K, s, 0, f4{Kk[0], Kk[1], Kk[2], Kk[3]});
+    rst4(r, K, s, 16, f4{Kk[4], Kk[5], Kk[6], Kk[7]});
+    rst2(r, k, s, 0, f2{kk[0], kk[1]});
   }
 };
 
@@ -323,11 +369,18 @@ __device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, float r
 // the tapes one iLQR solve works on
 template <bool TRACK>
 struct Solve {
-  Soa<4> X;   // [N+1][4][B] states + barrier state
-  Soa<2> U;   // [N][2][B] controls (in: warm start, out: plan)
-  Soa<4> Xr;  // TRACK: the nominal plan (x, y, theta used)
-  Soa<2> Ur;
+  Rsrc r;         // the workspace
+  RA XA, UA;      // this solve's tape records (states + barrier state, controls)
+  RA XRA, URA;    // TRACK: the nominal plan's records
   Gains G;
+  Soa<4> X;       // ABI [N+1][4][B] tape (written at the end of the solve)
+  Soa<2> U;       // ABI [N][2][B] controls (in: warm start, out: plan)
+  __device__ __forceinline__ f4 x(int k) const { return rld4(r, XA, k, 0); }
+  __device__ __forceinline__ f2 u(int k) const { return rld2(r, UA, k, 0); }
+  __device__ __forceinline__ void stx(int k, f4 v) const { rst4(r, XA, k, 0, v); }
+  __device__ __forceinline__ void stu(int k, f2 v) const { rst2(r, UA, k, 0, v); }
+  __device__ __forceinline__ f4 xr(int k) const { return rld4(r, XRA, k, 0); }
+  __device__ __forceinline__ f2 ur(int k) const { return rld2(r, URA, k, 0); }
 };
 
 struct StepIn {
@@ -338,28 +391,49 @@ struct StepIn {
 
 template <bool TRACK>
 __device__ __forceinline__ void load_step(StepIn& L, const Solve<TRACK>& S, int k) {
-  L.X0 = S.X.ld(k, 0);
-  L.X1 = S.X.ld(k, 1);
-  L.X2 = S.X.ld(k, 2);
-  L.X3 = S.X.ld(k, 3);
-  L.V0 = S.U.ld(k, 0);
-  L.V1 = S.U.ld(k, 1);
-  const float* q = S.G.K.p(k);
-  L.Ka = ld4(q);
-  L.Kb = ld4(q + 4);
-  L.kk = ld2(S.G.k.p(k));
+  const f4 X = S.x(k);
+  const f2 V = S.u(k);
+  L.X0 = X.x;
+  L.X1 = X.y;
+  L.X2 = X.z;
+  L.X3 = X.w;
+  L.V0 = V.x;
+  L.V1 = V.y;
+  L.Ka = rld4(S.r, S.G.K, k, 0);
+  L.Kb = rld4(S.r, S.G.K, k, 16);
+  L.kk = rld2(S.r, S.G.k, k, 0);
   if (TRACK) {
-    L.r0 = S.Xr.ld(k, 0);
-    L.r1 = S.Xr.ld(k, 1);
-    L.r2 = S.Xr.ld(k, 2);
-    L.q0 = S.Ur.ld(k, 0);
-    L.q1 = S.Ur.ld(k, 1);
+    const f4 R = S.xr(k);
+    const f2 Q = S.ur(k);
+    L.r0 = R.x;
+    L.r1 = R.y;
+    L.r2 = R.z;
+    L.q0 = Q.x;
+    L.q1 = Q.y;
   } else {
     L.r0 = L.r1 = L.r2 = L.q0 = L.q1 = 0.f;
   }
 }
 
-// iLQR start (init_tape): V = clamp(V_init), X = rollout(x0, V) and the alpha = 0 candidate's cost
+// the solved tape out to the ABI SoA arrays (X, U), once per solve
+__device__ __forceinline__ void copy_out(int N, const Rsrc& r, const RA& XA, const RA& UA, const Soa<4>& X,
+                                         const Soa<2>& U) {
+  for (int k = 0; k <= N; ++k) {
+    const f4 x = rld4(r, XA, k, 0);
+    X.st(k, 0, x.x);
+    X.st(k, 1, x.y);
+    X.st(k, 2, x.z);
+    X.st(k, 3, x.w);
+    if (k < N) {
+      const f2 u = rld2(r, UA, k, 0);
+      U.st(k, 0, u.x);
+      U.st(k, 1, u.y);
+    }
+  }
+}
+
+// iLQR start (init_tape): V = clamp(V_init) (the warm start, ABI SoA), X = rollout(x0, V) into this
+// solve's records, and the alpha = 0 candidate's cost
 template <bool TRACK, int M>
 __device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const float* x0, const Solve<TRACK>& S,
                                            bool want_cost) {
@@ -367,50 +441,37 @@ __device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const fl
   const int N = p.N;
   float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3];
   float Bc = barrier_at<M>(p, x0[0], x0[1]);
-  S.X.st(0, 0, s0);
-  S.X.st(0, 1, s1);
-  S.X.st(0, 2, s2);
-  S.X.st(0, 3, sb);
+  S.stx(0, f4{s0, s1, s2, sb});
   float J = 0.f;
-  float n0 = S.U.ld(0, 0), n1 = S.U.ld(0, 1), nr0 = 0.f, nr1 = 0.f, nr2 = 0.f, nq0 = 0.f, nq1 = 0.f;
+  float n0 = S.U.ld(0, 0), n1 = S.U.ld(0, 1);
+  f4 nR = f4{0.f, 0.f, 0.f, 0.f};
+  f2 nQ = f2{0.f, 0.f};
   if (TRACK) {
-    nr0 = S.Xr.ld(0, 0);
-    nr1 = S.Xr.ld(0, 1);
-    nr2 = S.Xr.ld(0, 2);
-    nq0 = S.Ur.ld(0, 0);
-    nq1 = S.Ur.ld(0, 1);
+    nR = S.xr(0);
+    nQ = S.ur(0);
   }
   for (int k = 0; k < N; ++k) {
-    const float v0 = n0, v1 = n1, r0 = nr0, r1 = nr1, r2 = nr2, q0 = nq0, q1 = nq1;
+    const float v0 = n0, v1 = n1;
+    const f4 R = nR;
+    const f2 Q = nQ;
     if (k + 1 < N) {
       n0 = S.U.ld(k + 1, 0);
       n1 = S.U.ld(k + 1, 1);
       if (TRACK) {
-        nr0 = S.Xr.ld(k + 1, 0);
-        nr1 = S.Xr.ld(k + 1, 1);
-        nr2 = S.Xr.ld(k + 1, 2);
-        nq0 = S.Ur.ld(k + 1, 0);
-        nq1 = S.Ur.ld(k + 1, 1);
+        nR = S.xr(k + 1);
+        nQ = S.ur(k + 1);
       }
     }
     const float u0 = vclamp(v0, p.umin0, p.umax0), u1 = vclamp(v1, p.umin1, p.umax1);
-    S.U.st(k, 0, u0);
-    S.U.st(k, 1, u1);
-    if (want_cost) J = J + stage<TRACK>(c, s0, s1, s2, sb, u0, u1, r0, r1, r2, q0, q1);
+    S.stu(k, f2{u0, u1});
+    if (want_cost) J = J + stage<TRACK>(c, s0, s1, s2, sb, u0, u1, R.x, R.y, R.z, Q.x, Q.y);
     fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
-    S.X.st(k + 1, 0, s0);
-    S.X.st(k + 1, 1, s1);
-    S.X.st(k + 1, 2, s2);
-    S.X.st(k + 1, 3, sb);
+    S.stx(k + 1, f4{s0, s1, s2, sb});
   }
   if (!want_cost) return 0.f;
-  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
-  if (TRACK) {
-    r0 = S.Xr.ld(N, 0);
-    r1 = S.Xr.ld(N, 1);
-    r2 = S.Xr.ld(N, 2);
-  }
-  return J + term<TRACK>(c, s0, s1, s2, sb, r0, r1, r2);
+  f4 R = f4{0.f, 0.f, 0.f, 0.f};
+  if (TRACK) R = S.xr(N);
+  return J + term<TRACK>(c, s0, s1, s2, sb, R.x, R.y, R.z);
 }
 
 // sparse augmented Jacobian (make_jac, core/systems/dubins_aug_jac.py:61-139)
@@ -441,12 +502,14 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
   const float lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
   const float luu[2] = {2.f * c.R0, 2.f * c.R1};
   const float pxx[4] = {2.f * c.Qf0, 2.f * c.Qf1, 2.f * c.Qf2, 2.f * c.qb};
-  const float xn0 = S.X.ld(N, 0), xn1 = S.X.ld(N, 1), xn2 = S.X.ld(N, 2), xnb = S.X.ld(N, 3);
+  const f4 XN = S.x(N);
+  const float xn0 = XN.x, xn1 = XN.y, xn2 = XN.z, xnb = XN.w;
   float d0, d1, d2;
   if (TRACK) {
-    d0 = xn0 - S.Xr.ld(N, 0);
-    d1 = xn1 - S.Xr.ld(N, 1);
-    d2 = xn2 - S.Xr.ld(N, 2);
+    const f4 RN = S.xr(N);
+    d0 = xn0 - RN.x;
+    d1 = xn1 - RN.y;
+    d2 = xn2 - RN.z;
   } else {
     d0 = xn0 - c.t0;
     d1 = xn1 - c.t1;
@@ -465,42 +528,33 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
   float dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
   bool ok = finite(R.Vx[0]) && finite(R.Vx[1]) && finite(R.Vx[2]) && finite(R.Vx[3]);
   // step inputs one step ahead
-  float nX0 = S.X.ld(N - 1, 0), nX1 = S.X.ld(N - 1, 1), nX2 = S.X.ld(N - 1, 2), nX3 = S.X.ld(N - 1, 3);
-  float nV0 = S.U.ld(N - 1, 0), nV1 = S.U.ld(N - 1, 1), nr0 = 0.f, nr1 = 0.f, nr2 = 0.f, nq0 = 0.f, nq1 = 0.f;
+  f4 nX = S.x(N - 1), nR = f4{0.f, 0.f, 0.f, 0.f};
+  f2 nV = S.u(N - 1), nQ = f2{0.f, 0.f};
   if (TRACK) {
-    nr0 = S.Xr.ld(N - 1, 0);
-    nr1 = S.Xr.ld(N - 1, 1);
-    nr2 = S.Xr.ld(N - 1, 2);
-    nq0 = S.Ur.ld(N - 1, 0);
-    nq1 = S.Ur.ld(N - 1, 1);
+    nR = S.xr(N - 1);
+    nQ = S.ur(N - 1);
   }
   for (int k = N - 1; k >= 0; --k) {
-    const float x0 = nX0, x1 = nX1, x2 = nX2, xb = nX3, u0 = nV0, u1 = nV1, r0 = nr0, r1 = nr1, r2 = nr2,
-                q0 = nq0, q1 = nq1;
+    const f4 X = nX, Rr = nR;
+    const f2 V = nV, Q = nQ;
     if (k > 0) {
-      nX0 = S.X.ld(k - 1, 0);
-      nX1 = S.X.ld(k - 1, 1);
-      nX2 = S.X.ld(k - 1, 2);
-      nX3 = S.X.ld(k - 1, 3);
-      nV0 = S.U.ld(k - 1, 0);
-      nV1 = S.U.ld(k - 1, 1);
+      nX = S.x(k - 1);
+      nV = S.u(k - 1);
       if (TRACK) {
-        nr0 = S.Xr.ld(k - 1, 0);
-        nr1 = S.Xr.ld(k - 1, 1);
-        nr2 = S.Xr.ld(k - 1, 2);
-        nq0 = S.Ur.ld(k - 1, 0);
-        nq1 = S.Ur.ld(k - 1, 1);
+        nR = S.xr(k - 1);
+        nQ = S.ur(k - 1);
       }
     }
+    const float x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w, u0 = V.x, u1 = V.y;
     float sn, cs;
     m_sincos(x2, &sn, &cs);
     float gxk, gyk;
     const float dBk = dbarrier(p, h_grad<M>(p, x0, x1, gxk, gyk));
     const Jac<float> J = jac(p, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
     if (TRACK) {
-      d0 = x0 - r0;
-      d1 = x1 - r1;
-      d2 = x2 - r2;
+      d0 = x0 - Rr.x;
+      d1 = x1 - Rr.y;
+      d2 = x2 - Rr.z;
     } else {
       d0 = x0 - c.t0;
       d1 = x1 - c.t1;
@@ -509,15 +563,15 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     const float lx[4] = {lxx[0] * d0, lxx[1] * d1, lxx[2] * d2, lxx[3] * xb};
     float lu[2];
     if (TRACK) {
-      lu[0] = luu[0] * (u0 - q0);
-      lu[1] = luu[1] * (u1 - q1);
+      lu[0] = luu[0] * (u0 - Q.x);
+      lu[1] = luu[1] * (u1 - Q.y);
     } else {
       lu[0] = luu[0] * u0;
       lu[1] = luu[1] * u1;
     }
     float Kk[8], kk[2];
     ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
-    S.G.store(k, Kk, kk);
+    S.G.store(S.r, k, Kk, kk);
     gxn = gxk;
     gyn = gyk;
     dBn = dBk;
@@ -703,9 +757,10 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   }
   float r0 = 0.f, r1 = 0.f, r2 = 0.f;
   if (TRACK) {
-    r0 = S.Xr.ld(N, 0);
-    r1 = S.Xr.ld(N, 1);
-    r2 = S.Xr.ld(N, 2);
+    const f4 RN = S.xr(N);
+    r0 = RN.x;
+    r1 = RN.y;
+    r2 = RN.z;
   }
   float Jc[2 * NPR];
   bool ok = true;
@@ -788,8 +843,9 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
   float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bc = Bc0;
   StepIn cur, nxt;
   Solve<false> T0;  // no references needed
-  T0.X = S.X;
-  T0.U = S.U;
+  T0.r = S.r;
+  T0.XA = S.XA;
+  T0.UA = S.UA;
   T0.G = S.G;
   load_step<false>(nxt, T0, 0);
   for (int k = 0; k < N; ++k) {
@@ -800,13 +856,9 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
     const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
     const float u0 = vclamp(cur.V0 + al * du0, p.umin0, p.umax0);
     const float u1 = vclamp(cur.V1 + al * du1, p.umin1, p.umax1);
-    S.U.st(k, 0, u0);
-    S.U.st(k, 1, u1);
+    S.stu(k, f2{u0, u1});
     fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
-    S.X.st(k + 1, 0, s0);
-    S.X.st(k + 1, 1, s1);
-    S.X.st(k + 1, 2, s2);
-    S.X.st(k + 1, 3, sb);
+    S.stx(k + 1, f4{s0, s1, s2, sb});
   }
 }
 
@@ -844,10 +896,14 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
   bool have_prev = false;
   float prev = 0.f;
   iters = 0;
+  int st = 0;
   pf.mark(ph);
   for (int it = 0; it < cf.max_iter; ++it) {
     iters = it + 1;
-    if (!backward<TRACK, M>(p, c, cf.reg, S)) return DTMPC_ST_NONFINITE;
+    if (!backward<TRACK, M>(p, c, cf.reg, S)) {
+      st = DTMPC_ST_NONFINITE;
+      break;
+    }
     pf.mark(ph + 1);
     float bestJ, al;
     const int best = line_search<TRACK, M, P>(p, c, cf, x0, Bc0, S, Jcur, h, bestJ, al);
@@ -855,7 +911,10 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
 #ifdef DTMPC_PROFILE
     ls_stat(TRACK ? 1 : 0, best, al, cf);
 #endif
-    if (best < 0) return DTMPC_ST_NONFINITE;
+    if (best < 0) {
+      st = DTMPC_ST_NONFINITE;
+      break;
+    }
     if (al != 0.f) commit<TRACK, M>(p, al, x0, Bc0, S);
     pf.mark(ph + 3);
     Jcur = bestJ;
@@ -863,15 +922,16 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
     have_prev = true;
     prev = bestJ;
   }
-  return 0;
+  copy_out(p.N, S.r, S.XA, S.UA, S.X, S.U);  // the tape as it stands (a failed solve's too)
+  return st;
 }
 
 // ---------------------------------------------------------------------------------------------
 // DDP sensitivity with the paper upper loss + DOC gradient (sens_traj<float, false, false, true>,
 // core/ddp.py:317-427, core/tube_mpc.py:915-976): acc = L, gQ(3), gR(2), gqb
 template <int M>
-__device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const Solve<true>& S, const Rec<8>& AB8,
-                                           const Rec<2>& AB2, float* acc) {
+__device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const Solve<true>& S, const RA& A8, const RA& A2,
+                                           float* acc) {
   const int N = p.N;
   const float lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
   const float luu[2] = {2.f * c.R0, 2.f * c.R1};
@@ -882,16 +942,24 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const So
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) R.Vxx[i][j] = i == j ? pxx[i] : 0.f;
-  const float xn0 = S.X.ld(N, 0), xn1 = S.X.ld(N, 1), xnb = S.X.ld(N, 3);
-  R.Vx[0] = 2.f * (xn0 - S.Xr.ld(N, 0));
-  R.Vx[1] = 2.f * (xn1 - S.Xr.ld(N, 1));
-  R.Vx[2] = 2.f * (S.X.ld(N, 2) - S.Xr.ld(N, 2));
-  R.Vx[3] = 2.f * xnb;
+  {
+    const f4 XN = S.x(N), RN = S.xr(N);
+    R.Vx[0] = 2.f * (XN.x - RN.x);
+    R.Vx[1] = 2.f * (XN.y - RN.y);
+    R.Vx[2] = 2.f * (XN.z - RN.z);
+    R.Vx[3] = 2.f * XN.w;
+  }
   float gxn, gyn;
-  float dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
+  float dBn;
+  {
+    const f4 XN = S.x(N);
+    dBn = dbarrier(p, h_grad<M>(p, XN.x, XN.y, gxn, gyn));
+  }
   for (int k = N - 1; k >= 0; --k) {
-    const float x0 = S.X.ld(k, 0), x1 = S.X.ld(k, 1), x2 = S.X.ld(k, 2), xb = S.X.ld(k, 3);
-    const float u0 = S.U.ld(k, 0), u1 = S.U.ld(k, 1);
+    const f4 X = S.x(k), Rr = S.xr(k);
+    const f2 V = S.u(k);
+    const float x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w;
+    const float u0 = V.x, u1 = V.y;
     float sn, cs;
     m_sincos(x2, &sn, &cs);
     float gxk, gyk;
@@ -906,9 +974,9 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const So
     const float tQu0 = J.b00 * tv[0] + J.b10 * tv[1] + J.b30 * tv[3];
     const float tQu1 = J.b21 * tv[2] + J.b31 * tv[3];
     float tQx[4];
-    tQx[0] = 2.f * (x0 - S.Xr.ld(k, 0)) + (tv[0] + J.a30 * tv[3]);
-    tQx[1] = 2.f * (x1 - S.Xr.ld(k, 1)) + (tv[1] + J.a31 * tv[3]);
-    tQx[2] = 2.f * (x2 - S.Xr.ld(k, 2)) + (J.a02 * tv[0] + J.a12 * tv[1] + tv[2] + J.a32 * tv[3]);
+    tQx[0] = 2.f * (x0 - Rr.x) + (tv[0] + J.a30 * tv[3]);
+    tQx[1] = 2.f * (x1 - Rr.y) + (tv[1] + J.a31 * tv[3]);
+    tQx[2] = 2.f * (x2 - Rr.z) + (J.a02 * tv[0] + J.a12 * tv[1] + tv[2] + J.a32 * tv[3]);
     tQx[3] = 2.f * xb + J.g * tv[3];
     const bool act0 = (u0 <= p.umin0 + p.active_tol) || (u0 >= p.umax0 - p.active_tol);
     const bool act1 = (u1 <= p.umin1 + p.active_tol) || (u1 >= p.umax1 - p.active_tol);
@@ -934,34 +1002,33 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const So
 #pragma unroll
       for (int j = 0; j < 4; ++j) R.Vxx[i][j] = Qxx[i][j] + (Qxu[i][0] * Kk[j] + Qxu[i][1] * Kk[4 + j]);
     }
-    S.G.store(k, Kk, kk);
-    float* q = AB8.p(k);
-    st4(q, f4{J.a02, J.a12, J.a30, J.a31});
-    st4(q + 4, f4{J.a32, J.b00, J.b10, J.b30});
-    st2(AB2.p(k), f2{J.b31, float((act0 ? 1 : 0) + (act1 ? 2 : 0))});
+    S.G.store(S.r, k, Kk, kk);
+    rst4(S.r, A8, k, 0, f4{J.a02, J.a12, J.a30, J.a31});
+    rst4(S.r, A8, k, 16, f4{J.a32, J.b00, J.b10, J.b30});
+    rst2(S.r, A2, k, 0, f2{J.b31, float((act0 ? 1 : 0) + (act1 ? 2 : 0))});
   }
   // forward (:413-425) fused with the upper loss and the DOC gradient
   float d[4] = {0.f, 0.f, 0.f, 0.f};
   float L1 = 0.f, L2 = 0.f, gQ0 = 0.f, gQ1 = 0.f, gQ2 = 0.f, gR0 = 0.f, gR1 = 0.f, gqb = 0.f;
   const float g = p.gamma, dt = p.dt;
   for (int k = 0; k < N; ++k) {
-    const float* gq = S.G.K.p(k);
-    const f4 Ka = ld4(gq), Kb = ld4(gq + 4);
-    const f2 kf = ld2(S.G.k.p(k));
-    const float* q = AB8.p(k);
-    const f4 A0 = ld4(q), A1 = ld4(q + 4);
-    const f2 A2 = ld2(AB2.p(k));
+    const f4 Ka = rld4(S.r, S.G.K, k, 0), Kb = rld4(S.r, S.G.K, k, 16);
+    const f2 kf = rld2(S.r, S.G.k, k, 0);
+    const f4 A0 = rld4(S.r, A8, k, 0), A1 = rld4(S.r, A8, k, 16);
+    const f2 A2r = rld2(S.r, A2, k, 0);
     const float a02 = A0.x, a12 = A0.y, a30 = A0.z, a31 = A0.w, a32 = A1.x, b00 = A1.y, b10 = A1.z, b30 = A1.w,
-                b31 = A2.x;
-    const int act = (int)A2.y;
+                b31 = A2r.x;
+    const int act = (int)A2r.y;
     const float v0 = (act & 1) ? 0.f : kf.x + (Ka.x * d[0] + Ka.y * d[1] + Ka.z * d[2] + Ka.w * d[3]);
     const float v1 = (act & 2) ? 0.f : kf.y + (Kb.x * d[0] + Kb.y * d[1] + Kb.z * d[2] + Kb.w * d[3]);
-    const float e0 = S.X.ld(k, 0) - S.Xr.ld(k, 0);
-    const float e1 = S.X.ld(k, 1) - S.Xr.ld(k, 1);
-    const float e2 = S.X.ld(k, 2) - S.Xr.ld(k, 2);
-    const float bb = S.X.ld(k, 3);
-    const float w0 = S.U.ld(k, 0) - S.Ur.ld(k, 0);
-    const float w1 = S.U.ld(k, 1) - S.Ur.ld(k, 1);
+    const f4 X = S.x(k), Rr = S.xr(k);
+    const f2 V = S.u(k), Q = S.ur(k);
+    const float e0 = X.x - Rr.x;
+    const float e1 = X.y - Rr.y;
+    const float e2 = X.z - Rr.z;
+    const float bb = X.w;
+    const float w0 = V.x - Q.x;
+    const float w1 = V.y - Q.y;
     L1 += e0 * e0 + e1 * e1 + e2 * e2;
     L2 += bb * bb;
     gQ0 += 2.f * e0 * d[0];
@@ -982,10 +1049,11 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const So
   bool ok = true;
 #pragma unroll
   for (int i = 0; i < 4; ++i) ok = ok && finite(d[i]);
-  const float e0 = S.X.ld(N, 0) - S.Xr.ld(N, 0);
-  const float e1 = S.X.ld(N, 1) - S.Xr.ld(N, 1);
-  const float e2 = S.X.ld(N, 2) - S.Xr.ld(N, 2);
-  const float bb = S.X.ld(N, 3);
+  const f4 XN = S.x(N), RN = S.xr(N);
+  const float e0 = XN.x - RN.x;
+  const float e1 = XN.y - RN.y;
+  const float e2 = XN.z - RN.z;
+  const float bb = XN.w;
   L1 += e0 * e0 + e1 * e1 + e2 * e2;
   L2 += bb * bb;
   acc[0] = L1 + L2;
@@ -1022,6 +1090,10 @@ __device__ __forceinline__ KArg* kargs() {
   return (KArg*)k;  // generic; the compiler infers the constant address space back (scalar loads)
 }
 
+#ifdef DTMPC_FAST_GLOBAL
+__device__ __forceinline__ const char* kargs_ws() { return (const char*)kargs()->a.work; }
+#endif
+
 #ifndef DTMPC_FAST_PIN
 #define DTMPC_FAST_PIN 1
 #endif
@@ -1046,16 +1118,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P, 
 tube_fast_kernel(FK kk) {
   (void)kk;  // read through kargs()
   __shared__ float red[kBlock / 64][DTMPC_TUBE_SUMS];
-  const int B = kargs()->a.B;
+  const int B = kargs()->a.B, Bc = kargs()->a.Bc, i0 = kargs()->a.i0;
   const int gl = blockIdx.x * kBlock + threadIdx.x;
-  const int i = P == 1 ? gl : (gl >> 1), h = P == 1 ? 0 : (gl & 1);
+  const int t = P == 1 ? gl : (gl >> 1), h = P == 1 ? 0 : (gl & 1);  // t: index in the chunk
+  const int i = i0 + t;                                                // index in the batch
   float acc[DTMPC_TUBE_SUMS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   Prof pf;
   pf.start();
-  if (i < B) {
+  if (t < Bc) {
     const size_t nb = (size_t)B;
     const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
     const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
+    const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * 8u, l16 = (unsigned)t * 16u, l32 = (unsigned)t * 32u;
     int st = 0, itn = 0, ita = 0;
     float x0, x1, x2, xb, y0, y1, y2, yb;
     {
@@ -1072,12 +1146,15 @@ tube_fast_kernel(FK kk) {
     {  // nominal MPC (fixed weights, :813-857)
       KArg* K = kargs();
       Solve<false> Sn;
+      Sn.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
+      Sn.XA = RA{K->a.oXn, cb * 16u, l16};
+      Sn.UA = RA{K->a.oUn, cb * 8u, l8};
+      Sn.XRA = Sn.XA;
+      Sn.URA = Sn.UA;
+      Sn.G.K = RA{K->a.oK, cb * 32u, l32};
+      Sn.G.k = RA{K->a.ok, cb * 8u, l8};
       Sn.X = Soa<4>{(char*)K->a.Xnom, 4u * bb, L};
       Sn.U = Soa<2>{(char*)K->a.Unom, 2u * bb, L};
-      Sn.G.K = Rec<8>{(char*)K->a.gK, bb * 8u, lo * 8u};
-      Sn.G.k = Rec<2>{(char*)K->a.gk, bb * 2u, lo * 2u};
-      Sn.Xr = Sn.X;
-      Sn.Ur = Sn.U;
       const FP p = phase_p<M>();
       const FCost cn = K->cn;
       const FIlqr cfn = K->cfn;
@@ -1098,12 +1175,15 @@ tube_fast_kernel(FK kk) {
     Solve<true> Sa;
     {  // ancillary MPC tracking the nominal plan (:863-909)
       KArg* K = kargs();
+      Sa.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
+      Sa.XA = RA{K->a.oXa, cb * 16u, l16};
+      Sa.UA = RA{K->a.oUa, cb * 8u, l8};
+      Sa.XRA = RA{K->a.oXn, cb * 16u, l16};
+      Sa.URA = RA{K->a.oUn, cb * 8u, l8};
+      Sa.G.K = RA{K->a.oK, cb * 32u, l32};
+      Sa.G.k = RA{K->a.ok, cb * 8u, l8};
       Sa.X = Soa<4>{(char*)K->a.Xaux, 4u * bb, L};
       Sa.U = Soa<2>{(char*)K->a.Uaux, 2u * bb, L};
-      Sa.Xr = Soa<4>{(char*)K->a.Xnom, 4u * bb, L};
-      Sa.Ur = Soa<2>{(char*)K->a.Unom, 2u * bb, L};
-      Sa.G.K = Rec<8>{(char*)K->a.gK, bb * 8u, lo * 8u};
-      Sa.G.k = Rec<2>{(char*)K->a.gk, bb * 2u, lo * 2u};
       const FP p = phase_p<M>();
       const FIlqr cfa = K->cfa;
       const float xa0[4] = {x0, x1, x2, xb};
@@ -1112,10 +1192,9 @@ tube_fast_kernel(FK kk) {
     pf.mark(8);
     {  // upper loss, DOC sensitivity and gradient (:915-976)
       KArg* K = kargs();
-      const Rec<8> AB8{(char*)K->a.ab8, bb * 8u, lo * 8u};
-      const Rec<2> AB2{(char*)K->a.ab2, bb * 2u, lo * 2u};
+      const RA A8{K->a.oA8, cb * 32u, l32}, A2{K->a.oA2, cb * 8u, l8};
       const FP p = phase_p<M>();
-      st |= sensitivity<M>(p, ca, Sa, AB8, AB2, acc);
+      st |= sensitivity<M>(p, ca, Sa, A8, A2, acc);
     }
     pf.mark(9);
     {  // plant step with disturbance, nominal propagation (:990-1001), log, warm-start shift
@@ -1205,7 +1284,7 @@ tube_fast_kernel(FK kk) {
     float v = 0.f;
 #pragma unroll
     for (int q = 0; q < kBlock / 64; ++q) v += red[q][threadIdx.x];
-    kargs()->a.partials[(size_t)blockIdx.x * DTMPC_TUBE_SUMS + threadIdx.x] = v;
+    kargs()->a.partials[((size_t)blockIdx.x + (size_t)i0 * P / kBlock) * DTMPC_TUBE_SUMS + threadIdx.x] = v;
   }
 }
 
@@ -1217,6 +1296,23 @@ tube_fast_kernel(FK kk) {
 // The fast kernel's configuration: f32, smooth-min over 1..8 obstacles, relaxed inverse barrier,
 // untightened h, nominal target cost without wrap, and six rolled-out candidates in both solves.
 // DTMPC_FAST=0 (environment, read at the call) forces the generic kernel (parity tests compare both).
+// trajectories per launch of the fast kernel: its workspace records (two tapes of (N+1) x 16 B + N x 8 B,
+// gains and sensitivity scratch of N x 40 B per trajectory) stay below 2^31 bytes, in workgroup multiples
+// (DTMPC_FAST_CHUNK, environment, read at each call: a smaller chunk, for the tests of the chunked launch)
+int64_t tube_fast_chunk(int N) {
+  const int64_t per = (int64_t)(N + 1) * 32 + (int64_t)N * 96;
+  int64_t c = ((int64_t)0x7fffffff / per) / kBlock * kBlock;
+  if (const char* e = getenv("DTMPC_FAST_CHUNK")) {
+    const int64_t v = atoll(e) / kBlock * kBlock;
+    if (v > 0 && v < c) c = v;
+  }
+  return c < kBlock ? kBlock : c;
+}
+size_t tube_fast_workspace_bytes(int N, int64_t B) {
+  const int64_t c = tube_fast_chunk(N), b = B < c ? B : c;
+  return (size_t)b * ((size_t)(N + 1) * 32 + (size_t)N * 96);
+}
+
 bool tube_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf) {
   const char* e = getenv("DTMPC_FAST");
   if (e && e[0] == '0' && e[1] == 0) return false;
@@ -1288,12 +1384,7 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
   a.Unom = (float*)S->Unom;
   a.Xaux = (float*)S->Xaux;
   a.Uaux = (float*)S->Uaux;
-  float* wk = (float*)S->work;  // 20 N B of the 30 N B floats of dtmpc_tube_workspace_bytes
-  const size_t nb = (size_t)B * N;
-  a.gK = wk;
-  a.gk = wk + 8 * nb;
-  a.ab8 = wk + 10 * nb;
-  a.ab2 = wk + 18 * nb;
+  a.work = (float*)S->work;
   a.theta = (const float*)S->theta;
   a.partials = (float*)S->partials;
   a.log = (float*)S->log;
@@ -1308,7 +1399,24 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     a.whi[f] = float(cf->w_high[f]);
   }
   const int lanes = S->lanes;
-  const dim3 grid = grid_for(B * lanes);
+  // the batch in chunks whose workspace records fit one buffer resource (< 2^31 bytes), each chunk a
+  // multiple of the workgroup size (its partial-sum rows follow the previous chunk's)
+  const int64_t chunk = tube_fast_chunk(N);
+  for (int64_t c0 = 0; c0 < B; c0 += chunk) {
+    const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
+    a.i0 = (int)c0;
+    a.Bc = (int)Bc;
+    const unsigned X = (unsigned)(Bc * (N + 1) * 16), U = (unsigned)(Bc * N * 8), K = (unsigned)(Bc * N * 32);
+    a.oXn = 0;
+    a.oXa = X;
+    a.oUn = 2 * X;
+    a.oUa = 2 * X + U;
+    a.oK = 2 * X + 2 * U;
+    a.ok = 2 * X + 2 * U + K;
+    a.oA8 = 2 * X + 3 * U + K;
+    a.oA2 = 2 * X + 3 * U + 2 * K;
+    a.wsz = 2 * X + 4 * U + 2 * K;
+    const dim3 grid = grid_for(Bc * lanes);
 #define FAST_CASE(m)                                                                                       \
   case m:                                                                                                  \
     if (lanes == 2)                                                                                        \
@@ -1316,15 +1424,16 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     else                                                                                                   \
       hipLaunchKernelGGL((fk::tube_fast_kernel<m, 1>), grid, dim3(kBlock), 0, st, kk);                   \
     break;
-  switch (sp->n_obstacles) {
+    switch (sp->n_obstacles) {
 #ifdef DTMPC_FAST_M_ONLY
-    FAST_CASE(DTMPC_FAST_M_ONLY)
+      FAST_CASE(DTMPC_FAST_M_ONLY)
 #else
-    FAST_CASE(1) FAST_CASE(2) FAST_CASE(3) FAST_CASE(4) FAST_CASE(5) FAST_CASE(6) FAST_CASE(7) FAST_CASE(8)
+      FAST_CASE(1) FAST_CASE(2) FAST_CASE(3) FAST_CASE(4) FAST_CASE(5) FAST_CASE(6) FAST_CASE(7) FAST_CASE(8)
 #endif
-    default: return set_err(DTMPC_ERR_BAD_ARG, "fast tube step: obstacle count not instantiated");
-  }
+      default: return set_err(DTMPC_ERR_BAD_ARG, "fast tube step: obstacle count not instantiated");
+    }
 #undef FAST_CASE
+  }
   return check_launch("tube_fast_kernel");
 }
 

@@ -621,7 +621,11 @@ int dtmpc_doc_grad(int dtype, int32_t horizon, int64_t B, const void* Xaux, cons
 
 size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
   size_t el = dtype == DTMPC_F64 ? 8 : 4;
-  return el * (size_t)horizon * 30 * (size_t)B;  // sensitivity K / kf / AB (SoA, 20) + iLQR gains (AoS, 10)
+  // generic kernel: sensitivity K / kf / AB (SoA, 20) + iLQR gains (AoS, 10) values per step;
+  // the f32 fast kernel: its per-lane records for one chunk (dtmpc_fast.hip)
+  const size_t gen = el * (size_t)horizon * 30 * (size_t)B;
+  const size_t fast = dtype == DTMPC_F32 ? tube_fast_workspace_bytes(horizon, B) : 0;
+  return gen > fast ? gen : fast;
 }
 
 int32_t dtmpc_tube_lanes(int64_t B) { return tube_lanes_default(B); }

@@ -113,7 +113,12 @@ def test_arguments_validated_before_any_device_call(lib):
     state = _abi.DtmpcTubeState()
     rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
     assert rc == _abi.ERR_BAD_ARG and b"same width" in lib.dtmpc_last_error()
-    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536) == 4 * 50 * 30 * 65536  # SoA scratch 20 + AoS gains 10
+    # f32: the larger of the generic kernel's scratch (30 values per step) and the fast kernel's per-lane
+    # records (two tapes of (N+1) x 16 B + N x 8 B, gains and sensitivity scratch of N x 40 B per trajectory)
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536) == max(4 * 50 * 30, 51 * 32 + 50 * 96) * 65536
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 65536) == 8 * 50 * 30 * 65536
+    # above 2^31 bytes of records the fast kernel runs in chunks: the workspace holds one chunk
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 1 << 22) == 4 * 50 * 30 * (1 << 22)
     assert lib.dtmpc_tube_partials_count(65536, 1) == 256
     assert lib.dtmpc_tube_partials_count(1000, 2) == 8
     assert lib.dtmpc_tube_partials_count(1000, 3) == 0

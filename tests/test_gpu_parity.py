@@ -556,6 +556,39 @@ def test_full_batch_properties(dev):
     assert bool((J1 <= J0 * (1 + 1e-5) + 1e-3).all())
 
 
+@pytest.mark.parametrize("lanes", ["1", "2"])
+def test_tube_step_fast_chunked_bitwise(dev, lanes, monkeypatch):
+    """The f32 fast kernel keeps its per-lane records in one buffer resource (< 2^31 bytes), so a batch
+    whose records exceed that runs in chunks of trajectories (dtmpc_fast.hip tube_fast_chunk).  Forcing
+    chunks of 256 (DTMPC_FAST_CHUNK) on a ragged batch of 700 = 256 + 256 + 188 must give bitwise the
+    single-launch results: states, tapes, log rows, partial sums and the shared theta."""
+    import dataclasses
+
+    from diff_tube_mpc_strict_pt.core import TubeMPC
+
+    monkeypatch.setenv("DTMPC_TUBE_LANES", lanes)
+    st = paper_setup()
+    st = dataclasses.replace(st, ilqr_nom=dataclasses.replace(st.ilqr_nom, tol=-1.0),
+                             ilqr_aux=dataclasses.replace(st.ilqr_aux, tol=-1.0))
+    B = 700
+    rng = np.random.default_rng(5)
+    x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(np.float32)
+    names = ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux", "theta", "status", "log", "partials")
+    runs = []
+    for chunk in (None, "256"):
+        if chunk:
+            monkeypatch.setenv("DTMPC_FAST_CHUNK", chunk)
+        m = TubeMPC(st, batch=B, device=dev, dtype=torch.float32, disturbance="philox", seed=4, write_log=True)
+        m.reset(_t(x, torch.float32, dev))
+        m.step()
+        m.step()
+        torch.cuda.synchronize()
+        runs.append({k: getattr(m, k).clone() for k in names if getattr(m, k, None) is not None})
+    assert (runs[0]["status"] == 0).all()
+    for k in runs[0]:
+        assert torch.equal(runs[0][k], runs[1][k]), k
+
+
 @pytest.mark.parametrize("tag", ["f64", "f32"])
 def test_status_and_errors(dev, tag):
     """Non-finite inputs raise FloatingPointError (core/ddp.py:138-159); bad arguments ValueError."""
