@@ -675,6 +675,21 @@ __device__ __forceinline__ void solve_reduced(const LU2<T>& f, T m00, T m11, boo
   }
 }
 
+// all of K[8], k[2] finite.  f32: one NaN-propagating max of the magnitudes (v_maximum3_f32) and a
+// single class test instead of ten.
+__device__ __forceinline__ bool finite10(const float* K, const float* k) {
+  float m = __builtin_elementwise_maximum(__builtin_fabsf(k[0]), __builtin_fabsf(k[1]));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m = __builtin_elementwise_maximum(m, __builtin_fabsf(K[j]));
+  return finite(m);
+}
+__device__ __forceinline__ bool finite10(const double* K, const double* k) {
+  bool ok = finite(k[0]) && finite(k[1]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ok = ok && finite(K[j]);
+  return ok;
+}
+
 // ---------------------------------------------------------------------------------------------
 // iLQR backward step with the sparse Jacobian (core/ddp.py:213-254).
 // l_xx = diag(lxx0..3), l_uu = diag(luu0,1), l_ux = 0.  Vx/Vxx are updated in place.
@@ -751,9 +766,7 @@ __device__ __forceinline__ bool riccati_step(const Jac<T>& J, const T* lx, const
     kff[0] = -x0;
     kff[1] = -x1;
   }
-  bool ok = finite(kff[0]) && finite(kff[1]);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ok = ok && finite(K[j]);
+  bool ok = finite10(K, kff);
   // V_x = Q_x + K^T Q_uu k + K^T Q_u + Q_xu k  ;  V_xx = Q_xx + K^T Q_uu K + K^T Q_ux + Q_xu K
   // (unregularised Q_uu, :251-252)
   T KQ[4][2];

@@ -39,6 +39,7 @@ struct FP {
   int N;
   float dt, umin0, umin1, umax0, umax1, active_tol;
   float neg_beta, neg_inv_beta;
+  float nbl2e;  // neg_beta * log2(e): exp(-beta h_i - zmax) = exp2(fma(h_i, nbl2e, -zmax log2(e)))
   float a, eps, gamma, inv_a, a2, a3, inv_a2;
   float cx[8], cy[8], r2[8];
 };
@@ -216,6 +217,8 @@ __device__ __forceinline__ float vclamp(float v, float lo, float hi) {
 __device__ __forceinline__ f2 vclamp(f2 v, float lo, float hi) { return f2{vclamp(v.x, lo, hi), vclamp(v.y, lo, hi)}; }
 __device__ __forceinline__ float vmaxnan(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 __device__ __forceinline__ float vexp(float x) { return m_exp(x); }
+__device__ __forceinline__ float vexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ f2 vexp2(f2 x) { return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; }
 __device__ __forceinline__ f2 vexp(f2 x) { return pk_exp(x); }
 __device__ __forceinline__ float vlog(float x) { return m_log(x); }
 __device__ __forceinline__ f2 vlog(f2 x) { return pk_log(x); }
@@ -271,9 +274,10 @@ __device__ __forceinline__ V h_sm(const FP& p, V px, V py) {
     hm = i == 0 ? hi[0] : vmin(hm, hi[i]);
   }
   const V zmax = p.neg_beta * hm;
+  const V zl = zmax * 1.44269504088896341f;
   V se = 0.f;
 #pragma unroll
-  for (int i = 0; i < M; ++i) se += vexp(p.neg_beta * hi[i] - zmax);
+  for (int i = 0; i < M; ++i) se += vexp2(__builtin_elementwise_fma(hi[i], V(p.nbl2e), -zl));
   return p.neg_inv_beta * (zmax + vlog(se));
 }
 
@@ -281,18 +285,20 @@ __device__ __forceinline__ V h_sm(const FP& p, V px, V py) {
 template <int M>
 __device__ __forceinline__ float h_grad(const FP& p, float px, float py, float& gx, float& gy) {
 #pragma clang fp contract(off)
-  float z[M], zmax = 0.f;
+  float z[M], hh[M], zmax = 0.f;
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     const float dx = px - p.cx[i];
     const float dy = py - p.cy[i];
-    z[i] = p.neg_beta * (dx * dx + dy * dy - p.r2[i]);
+    hh[i] = dx * dx + dy * dy - p.r2[i];
+    z[i] = p.neg_beta * hh[i];
     zmax = (i == 0 || z[i] > zmax) ? z[i] : zmax;
   }
+  const float zl = zmax * 1.44269504088896341f;
   float se = 0.f, sx = 0.f, sy = 0.f;
 #pragma unroll
   for (int i = 0; i < M; ++i) {
-    const float e = m_exp(z[i] - zmax);
+    const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(hh[i], p.nbl2e, -zl));
     se += e;
     sx += e * (2.f * (px - p.cx[i]));
     sy += e * (2.f * (py - p.cy[i]));
@@ -516,14 +522,14 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     d2 = xn2 - c.t2;
   }
   Riccati<float> R;
-  R.Vx[0] = pxx[0] * d0;
-  R.Vx[1] = pxx[1] * d1;
-  R.Vx[2] = pxx[2] * d2;
-  R.Vx[3] = pxx[3] * xnb;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) R.Vxx[i][j] = i == j ? pxx[i] : 0.f;
+  R.Vx[0] = pxx[0] * d0;
+  R.Vx[1] = pxx[1] * d1;
+  R.Vx[2] = pxx[2] * d2;
+  R.Vx[3] = pxx[3] * xnb;
   float gxn, gyn;
   float dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
   bool ok = finite(R.Vx[0]) && finite(R.Vx[1]) && finite(R.Vx[2]) && finite(R.Vx[3]);
@@ -683,14 +689,17 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
       hi[i][q] = dx * dx + dy * dy - p.r2[i];
       hm[q] = i == 0 ? hi[0][q] : vmin(hm[q], hi[i][q]);
     }
-  f2 zmax[NPR], se[NPR], z[NPR];
+  f2 zmax[NPR], zl[NPR], se[NPR], z[NPR];
 #pragma unroll
-  for (int q = 0; q < NPR; ++q) zmax[q] = p.neg_beta * hm[q];
+  for (int q = 0; q < NPR; ++q) {
+    zmax[q] = p.neg_beta * hm[q];
+    zl[q] = zmax[q] * 1.44269504088896341f;
+  }
 #pragma unroll
   for (int i = 0; i < M; ++i)
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
-      const f2 e = vexp(p.neg_beta * hi[i][q] - zmax[q]);
+      const f2 e = vexp2(__builtin_elementwise_fma(hi[i][q], f2(p.nbl2e), -zl[q]));
       se[q] = i == 0 ? e : se[q] + e;  // = 0 + e_0 + ...: e_0 >= 0, so 0 + e_0 == e_0 bitwise
     }
 #pragma unroll
@@ -1130,6 +1139,7 @@ tube_fast_kernel(FK kk) {
     const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
     const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
     const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * 8u, l16 = (unsigned)t * 16u, l32 = (unsigned)t * 32u;
+
     int st = 0, itn = 0, ita = 0;
     float x0, x1, x2, xb, y0, y1, y2, yb;
     {
@@ -1353,6 +1363,7 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
   p.active_tol = s.active_tol;
   p.neg_beta = s.neg_beta;
   p.neg_inv_beta = s.neg_inv_beta;
+  p.nbl2e = s.neg_beta * 1.44269504088896341f;
   p.eps = s.eps;
   p.gamma = s.gamma;
   // alpha_eff = max(alpha, eps) and the constants of the relaxed branch, in f32 as the device forms them
