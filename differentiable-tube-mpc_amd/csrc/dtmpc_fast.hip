@@ -540,17 +540,7 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     nR = S.xr(N - 1);
     nQ = S.ur(N - 1);
   }
-  for (int k = N - 1; k >= 0; --k) {
-    const f4 X = nX, Rr = nR;
-    const f2 V = nV, Q = nQ;
-    if (k > 0) {
-      nX = S.x(k - 1);
-      nV = S.u(k - 1);
-      if (TRACK) {
-        nR = S.xr(k - 1);
-        nQ = S.ur(k - 1);
-      }
-    }
+  auto step = [&](const f4& X, const f2& V, const f4& Rr, const f2& Q, int k) {
     const float x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w, u0 = V.x, u1 = V.y;
     float sn, cs;
     m_sincos(x2, &sn, &cs);
@@ -581,6 +571,19 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     gxn = gxk;
     gyn = gyk;
     dBn = dBk;
+  };
+  for (int k = N - 1; k >= 0; --k) {
+    const f4 X = nX, Rr = nR;
+    const f2 V = nV, Q = nQ;
+    if (k > 0) {
+      nX = S.x(k - 1);
+      nV = S.u(k - 1);
+      if (TRACK) {
+        nR = S.xr(k - 1);
+        nQ = S.ur(k - 1);
+      }
+    }
+    step(X, V, Rr, Q, k);
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) ok = ok && finite(R.Vx[i]);
@@ -843,6 +846,9 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   return ok ? best : -1;
 }
 
+#ifndef DTMPC_FAST_CM_DEPTH2
+#define DTMPC_FAST_CM_DEPTH2 1  // 0: one step of prefetch lead (measured 3 % slower)
+#endif
 // materialise the chosen candidate in place (commit_candidate): same arithmetic as its lane of the
 // line search; the old X[k+1] is read (prefetched) before it is overwritten
 template <bool TRACK, int M>
@@ -850,16 +856,12 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
   DTMPC_NOCONTRACT
   const int N = p.N;
   float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bc = Bc0;
-  StepIn cur, nxt;
   Solve<false> T0;  // no references needed
   T0.r = S.r;
   T0.XA = S.XA;
   T0.UA = S.UA;
   T0.G = S.G;
-  load_step<false>(nxt, T0, 0);
-  for (int k = 0; k < N; ++k) {
-    cur = nxt;
-    if (k + 1 < N) load_step<false>(nxt, T0, k + 1);
+  auto step = [&](const StepIn& cur, int k) {
     const float e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
     const float du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
     const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
@@ -868,7 +870,38 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
     S.stu(k, f2{u0, u1});
     fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
     S.stx(k + 1, f4{s0, s1, s2, sb});
+  };
+#if DTMPC_FAST_CM_DEPTH2
+  // four step buffers in rotation, each refilled two steps before it is used (the commit's step is
+  // short, ~250 instructions: one step of lead does not cover an HBM read).  A refill of step j reads
+  // the OLD X[j] before step j-1 overwrites it (issued earlier in program order).
+  const int N1 = N - 1;
+  auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
+  StepIn A, Bq, Cq, Dq;
+  load_step<false>(A, T0, 0);
+  load_step<false>(Bq, T0, ix(1));
+  for (int k = 0; k < N; k += 4) {
+    load_step<false>(Cq, T0, ix(k + 2));
+    step(A, k);
+    if (k + 1 >= N) break;
+    load_step<false>(Dq, T0, ix(k + 3));
+    step(Bq, k + 1);
+    if (k + 2 >= N) break;
+    load_step<false>(A, T0, ix(k + 4));
+    step(Cq, k + 2);
+    if (k + 3 >= N) break;
+    load_step<false>(Bq, T0, ix(k + 5));
+    step(Dq, k + 3);
   }
+#else
+  StepIn cur, nxt;
+  load_step<false>(nxt, T0, 0);
+  for (int k = 0; k < N; ++k) {
+    cur = nxt;
+    if (k + 1 < N) load_step<false>(nxt, T0, k + 1);
+    step(cur, k);
+  }
+#endif
 }
 
 #ifdef DTMPC_PROFILE
