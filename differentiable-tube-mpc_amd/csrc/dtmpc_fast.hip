@@ -371,6 +371,20 @@ __device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, float r
   return sq + c.qb * (b * b);
 }
 
+// K_row . e of the feedback du = k + K (x - X_k) (core/ddp.py:267-268), as an fma chain: the
+// reference's K @ dx is a BLAS/ATen matrix-vector product whose summation and fusion are its own; the
+// line search and the commit use this same chain, so a committed tape is the candidate priced.
+#ifndef DTMPC_FAST_KFMA
+#define DTMPC_FAST_KFMA 1
+#endif
+template <class V>
+__device__ __forceinline__ V kdot(const f4& K, V e0, V e1, V e2, V e3) {
+  V t = K.x * e0;
+  t = __builtin_elementwise_fma(V(K.y), e1, t);
+  t = __builtin_elementwise_fma(V(K.z), e2, t);
+  return __builtin_elementwise_fma(V(K.w), e3, t);
+}
+
 // ---------------------------------------------------------------------------------------------
 // the tapes one iLQR solve works on
 template <bool TRACK>
@@ -659,8 +673,13 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
     const f2 e0 = C.a0[q] - s.X0, e1 = C.a1[q] - s.X1, e2 = C.a2[q] - s.X2, e3 = C.ab[q] - s.X3;
+#if DTMPC_FAST_KFMA
+    const f2 du0 = s.kk.x + kdot(s.Ka, e0, e1, e2, e3);
+    const f2 du1 = s.kk.y + kdot(s.Kb, e0, e1, e2, e3);
+#else
     const f2 du0 = s.kk.x + (s.Ka.x * e0 + s.Ka.y * e1 + s.Ka.z * e2 + s.Ka.w * e3);
     const f2 du1 = s.kk.y + (s.Kb.x * e0 + s.Kb.y * e1 + s.Kb.z * e2 + s.Kb.w * e3);
+#endif
     u0[q] = s.V0 + C.al[q] * du0;
     u1[q] = s.V1 + C.al[q] * du1;
   }
@@ -863,8 +882,13 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
   T0.G = S.G;
   auto step = [&](const StepIn& cur, int k) {
     const float e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
+#if DTMPC_FAST_KFMA
+    const float du0 = cur.kk.x + kdot(cur.Ka, e0, e1, e2, e3);
+    const float du1 = cur.kk.y + kdot(cur.Kb, e0, e1, e2, e3);
+#else
     const float du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
     const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
+#endif
     const float u0 = vclamp(cur.V0 + al * du0, p.umin0, p.umax0);
     const float u1 = vclamp(cur.V1 + al * du1, p.umin1, p.umax1);
     S.stu(k, f2{u0, u1});
