@@ -33,6 +33,34 @@ __global__ void __launch_bounds__(kBlock) dbas_init_kernel(DSpec<T> s, int B, co
   b[i] = barrier_of_state(s, x[i], x[(size_t)B + i]);
 }
 
+// episode start of the fused closed loop in one launch (core/tube_mpc.py:770-779): x = xbar = x0 (given
+// trajectory-major [B][3], the reference's layout), b = bbar = B(h(x0)), zero warm starts (both
+// [N][2][B] tapes: each lane clears its own column), status 0; lane 0 restores theta and clears the
+// momentum
+template <typename T>
+__global__ void __launch_bounds__(kBlock) tube_reset_kernel(DSpec<T> s, int B, const T* x0, T* x, T* b, T* xbar,
+                                                            T* bbar, T* Unom, T* Uaux, int* status,
+                                                            const T* theta0, T* theta, T* vel) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i == 0)
+    for (int j = 0; j < 6; ++j) {
+      theta[j] = theta0[j];
+      vel[j] = T(0);
+    }
+  if (i >= B) return;
+  const size_t nb = (size_t)B;
+  const T p0 = x0[3 * (size_t)i], p1 = x0[3 * (size_t)i + 1], p2 = x0[3 * (size_t)i + 2];
+  x[i] = xbar[i] = p0;
+  x[nb + i] = xbar[nb + i] = p1;
+  x[2 * nb + i] = xbar[2 * nb + i] = p2;
+  b[i] = bbar[i] = barrier_of_state(s, p0, p1);
+  for (int r = 0; r < 2 * s.N; ++r) {
+    Unom[r * nb + i] = T(0);
+    Uaux[r * nb + i] = T(0);
+  }
+  status[i] = 0;
+}
+
 // dense A [N][16], Bm [N][8], lx [N+1][4], lu [N][2] (dubins_augmented_jacobian + cost derivs)
 template <typename T>
 __global__ void __launch_bounds__(kBlock) linearize_kernel(DSpec<T> s, DCost<T> c, int B,
@@ -535,6 +563,28 @@ int dtmpc_dbas_init(int dtype, const dtmpc_spec* spec, int64_t B, const void* x,
   else
     return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
   return check_launch("dbas_init_kernel");
+}
+
+int dtmpc_tube_reset(int dtype, const dtmpc_spec* spec, int64_t B, const void* x0, const dtmpc_tube_state* S,
+                     const void* theta0, void* theta, void* vel, void* stream) {
+  int e = check_spec(spec, B);
+  if (e) return e;
+  if (!x0 || !S || !theta0 || !theta || !vel) return set_err(DTMPC_ERR_BAD_ARG, "NULL argument");
+  if (!S->x || !S->b || !S->xbar || !S->bbar || !S->Unom || !S->Uaux || !S->status)
+    return set_err(DTMPC_ERR_BAD_ARG, "NULL state array");
+  hipStream_t st = (hipStream_t)stream;
+#define RESET(T)                                                                                          \
+  hipLaunchKernelGGL(tube_reset_kernel<T>, grid_for(B), dim3(kBlock), 0, st, make_spec<T>(*spec), (int)B,   \
+                     (const T*)x0, (T*)S->x, (T*)S->b, (T*)S->xbar, (T*)S->bbar, (T*)S->Unom, (T*)S->Uaux,   \
+                     S->status, (const T*)theta0, (T*)theta, (T*)vel)
+  if (dtype == DTMPC_F32)
+    RESET(float);
+  else if (dtype == DTMPC_F64)
+    RESET(double);
+  else
+    return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+#undef RESET
+  return check_launch("tube_reset_kernel");
 }
 
 int dtmpc_linearize(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, int64_t B,

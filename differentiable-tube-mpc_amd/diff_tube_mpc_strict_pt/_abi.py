@@ -190,6 +190,7 @@ PROTOTYPES = {
         C.c_int,
         [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcTubeCfg), I64, I64, I64, C.POINTER(DtmpcTubeState), P, P],
     ),
+    "dtmpc_tube_reset": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), I64, P, C.POINTER(DtmpcTubeState), P, P, P, P]),
     "dtmpc_partials_reduce": (C.c_int, [C.c_int, I64, P, P, P]),
     "dtmpc_theta_update": (C.c_int, [C.c_int, C.POINTER(DtmpcAdaptCfg), C.c_double, P, P, P, P]),
     "dtmpc_sensitivity_upper_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64]),

@@ -169,6 +169,15 @@ class TubeMPC:
         warm starts default to zero; theta and momentum restart from the setup."""
         if x0.shape != (self.B, 3):
             raise ValueError(f"x0 must be [{self.B}, 3]")
+        if U_nom0 is None and U_aux0 is None:
+            # the whole episode start in one launch (dtmpc_tube_reset)
+            x0c = x0.to(device=self.device, dtype=self.dtype).contiguous()
+            _lib.check(self.lib.dtmpc_tube_reset(self._dt, C.byref(self.spec), self.B, x0c.data_ptr(),
+                                                 C.byref(self.state), self._theta0.data_ptr(),
+                                                 self.theta.data_ptr(), self.vel.data_ptr(), self._stream()),
+                       "dtmpc_tube_reset")
+            self.t = 0
+            return
         xs = x0.to(device=self.device, dtype=self.dtype).t().contiguous()
         self.x.copy_(xs)
         self.xbar.copy_(xs)

@@ -254,6 +254,14 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
                     int64_t global_offset, int64_t step, const dtmpc_tube_state* state,
                     const void* w, void* stream);
 
+/* Episode start of the fused closed loop in one launch (core/tube_mpc.py:770-779; the reference's
+ * run_closed_loop_experiment sets x = x_bar = x0, b = b_bar = B(h(x0)), zero warm starts and its
+ * initial adaptation weights): x0 [B][3] trajectory-major; writes state->x, xbar [3][B], b, bbar [B],
+ * Unom, Uaux [N][2][B] (zero), status [B] (zero), theta [6] = theta0 [6] and vel [6] = 0. */
+int dtmpc_tube_reset(int dtype, const dtmpc_spec* spec, int64_t B, const void* x0,
+                     const dtmpc_tube_state* state, const void* theta0, void* theta, void* vel,
+                     void* stream);
+
 /* Fixed-order sum of the per-workgroup partial records: sums [8] (L, gQ(3), gR(2), gqb, count). */
 int dtmpc_partials_reduce(int dtype, int64_t n_partials, const void* partials, void* sums,
                           void* stream);

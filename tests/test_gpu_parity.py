@@ -556,6 +556,38 @@ def test_full_batch_properties(dev):
     assert bool((J1 <= J0 * (1 + 1e-5) + 1e-3).all())
 
 
+@pytest.mark.parametrize("tag", ["f64", "f32"])
+def test_tube_reset_fused_matches_stepwise(dev, tag):
+    """dtmpc_tube_reset (the episode start in one launch) writes exactly what the step-by-step reset
+    does (copies, dtmpc_dbas_init, zero warm starts, theta0, zero momentum and status), from a dirty
+    state."""
+    from diff_tube_mpc_strict_pt.core import TubeMPC
+
+    npdt, tdt = DT[tag]
+    st = paper_setup()
+    B = 333
+    rng = np.random.default_rng(2)
+    x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(npdt)
+    N = st.problem.horizon
+    names = ("x", "b", "xbar", "bbar", "Unom", "Uaux", "theta", "vel", "status")
+    outs = []
+    for fused in (True, False):
+        m = TubeMPC(st, batch=B, device=dev, dtype=tdt, disturbance="philox", seed=1)
+        m.reset(_t(x, tdt, dev))
+        m.step()
+        m.status.fill_(3)
+        m.vel.fill_(1.0)
+        if fused:
+            m.reset(_t(x, tdt, dev))
+        else:
+            z = torch.zeros(B, N, 2, dtype=tdt, device=dev)
+            m.reset(_t(x, tdt, dev), U_nom0=z, U_aux0=z)
+        torch.cuda.synchronize()
+        outs.append({k: getattr(m, k).clone() for k in names})
+    for k in names:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
 @pytest.mark.parametrize("lanes", ["1", "2"])
 def test_tube_step_fast_chunked_bitwise(dev, lanes, monkeypatch):
     """The f32 fast kernel keeps its per-lane records in one buffer resource (< 2^31 bytes), so a batch
