@@ -515,6 +515,137 @@ __device__ __forceinline__ Jac<float> jac(const FP& p, float sn, float cs, float
   return J;
 }
 
+// iLQR backward step (core/ddp.py:213-254) on the sparse Jacobian with the 4 x 4 blocks held as rows of
+// column PAIRS, so that most of the recursion issues as packed f32 (two columns per instruction):
+// P = A^T V, Q_xx = P A, S = B^T V, Q_ux = S A row by row; the 2 x 2 LU solve (partial pivoting, as
+// torch.linalg.solve) on pairs of right-hand-side columns; V_x and V_xx updates as fma chains.  The
+// same products as riccati_step (the reference's dense update restricted to the nonzeros of A, B),
+// contracted and grouped for pairs: V_xx' = Q_xx + K^T Q_uu K + K^T Q_ux + Q_xu K accumulated term by
+// term in one fma chain per pair.
+#ifndef DTMPC_FAST_RICPK
+#define DTMPC_FAST_RICPK 1
+#endif
+struct RicP {
+  f2 V[4][2];  // V_xx: row i, columns (0, 1) and (2, 3)
+  f2 Vx[2];    // (V_x0, V_x1), (V_x2, V_x3)
+};
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 bc(float v) { return f2{v, v}; }
+
+__device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx, const float* lu, const float* lxx,
+                                           const float* luu, float reg, RicP& R, float* K, float* kff) {
+  const float a02 = J.a02, a12 = J.a12, a30 = J.a30, a31 = J.a31, a32 = J.a32, g = J.g;
+  const float b00 = J.b00, b10 = J.b10, b21 = J.b21, b30 = J.b30, b31 = J.b31;
+  const f2 A3 = f2{a30, a31};
+  const float vx0 = R.Vx[0].x, vx1 = R.Vx[0].y, vx2 = R.Vx[1].x, vx3 = R.Vx[1].y;
+  // Q_x = l_x + A^T V_x ; Q_u = l_u + B^T V_x
+  const f2 Qx01 = f2{lx[0], lx[1]} + fma2(A3, bc(vx3), R.Vx[0]);
+  const float Qx2 = lx[2] + (a02 * vx0 + a12 * vx1 + vx2 + a32 * vx3);
+  const float Qx3 = lx[3] + g * vx3;
+  const float Qu0 = lu[0] + (b00 * vx0 + b10 * vx1 + b30 * vx3);
+  const float Qu1 = lu[1] + (b21 * vx2 + b31 * vx3);
+  // P = A^T V_xx
+  f2 P[4][2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    P[0][c] = fma2(bc(a30), R.V[3][c], R.V[0][c]);
+    P[1][c] = fma2(bc(a31), R.V[3][c], R.V[1][c]);
+    P[2][c] = fma2(bc(a32), R.V[3][c], fma2(bc(a12), R.V[1][c], fma2(bc(a02), R.V[0][c], R.V[2][c])));
+    P[3][c] = bc(g) * R.V[3][c];
+  }
+  // Q_xx = P A + l_xx
+  f2 Q[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float p0 = P[i][0].x, p1 = P[i][0].y, p2 = P[i][1].x, p3 = P[i][1].y;
+    Q[i][0] = fma2(A3, bc(p3), P[i][0]);
+    Q[i][1] = f2{a02 * p0 + a12 * p1 + p2 + a32 * p3, g * p3};
+  }
+  Q[0][0].x = lxx[0] + Q[0][0].x;
+  Q[1][0].y = lxx[1] + Q[1][0].y;
+  Q[2][1].x = lxx[2] + Q[2][1].x;
+  Q[3][1].y = lxx[3] + Q[3][1].y;
+  // S = B^T V_xx ; Q_ux = S A ; Q_uu = l_uu + S B
+  f2 S[2][2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    S[0][c] = fma2(bc(b30), R.V[3][c], fma2(bc(b10), R.V[1][c], bc(b00) * R.V[0][c]));
+    S[1][c] = fma2(bc(b31), R.V[3][c], bc(b21) * R.V[2][c]);
+  }
+  f2 Qux[2][2];
+  float Quu[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const float s0 = S[a][0].x, s1 = S[a][0].y, s2 = S[a][1].x, s3 = S[a][1].y;
+    Qux[a][0] = fma2(A3, bc(s3), S[a][0]);
+    Qux[a][1] = f2{a02 * s0 + a12 * s1 + s2 + a32 * s3, g * s3};
+    Quu[a][0] = s0 * b00 + s1 * b10 + s3 * b30;
+    Quu[a][1] = s2 * b21 + s3 * b31;
+  }
+  Quu[0][0] = luu[0] + Quu[0][0];
+  Quu[1][1] = luu[1] + Quu[1][1];
+  // gains with the regularised Q_uu (:239-249): LU with partial pivoting, K = -x, k = -x
+  const LU2<float> f = lu2(Quu[0][0] + reg, Quu[0][1], Quu[1][0], Quu[1][1] + reg);
+  f2 Kp[2][2];  // K row a, columns (0, 1) and (2, 3)
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const f2 r0 = Qux[0][c], r1 = Qux[1][c];
+    const f2 p0 = f2{f.sw ? r1.x : r0.x, f.sw ? r1.y : r0.y}, p1 = f2{f.sw ? r0.x : r1.x, f.sw ? r0.y : r1.y};
+    const f2 y1 = p1 - bc(f.l) * p0;
+    Kp[1][c] = y1 * bc(-f.inv11);
+    Kp[0][c] = (p0 + bc(f.a01) * Kp[1][c]) * bc(-f.inv00);
+  }
+  {
+    const float p0 = f.sw ? Qu1 : Qu0, p1 = f.sw ? Qu0 : Qu1;
+    const float y1 = p1 - f.l * p0;
+    kff[1] = y1 * -f.inv11;
+    kff[0] = (p0 + f.a01 * kff[1]) * -f.inv00;
+  }
+  K[0] = Kp[0][0].x;
+  K[1] = Kp[0][0].y;
+  K[2] = Kp[0][1].x;
+  K[3] = Kp[0][1].y;
+  K[4] = Kp[1][0].x;
+  K[5] = Kp[1][0].y;
+  K[6] = Kp[1][1].x;
+  K[7] = Kp[1][1].y;
+  const bool ok = finite10(K, kff);
+  // KQ = K^T Q_uu (unregularised, :251-252), pairs over i: KQa[c] = (KQ[2c][a], KQ[2c+1][a])
+  f2 KQ0[2], KQ1[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    KQ0[c] = fma2(bc(Quu[1][0]), Kp[1][c], bc(Quu[0][0]) * Kp[0][c]);
+    KQ1[c] = fma2(bc(Quu[1][1]), Kp[1][c], bc(Quu[0][1]) * Kp[0][c]);
+  }
+  // V_x = Q_x + K^T Q_uu k + K^T Q_u + Q_xu k
+  const f2 Qxp[2] = {Qx01, f2{Qx2, Qx3}};
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const f2 t1 = fma2(KQ1[c], bc(kff[1]), KQ0[c] * bc(kff[0]));
+    const f2 t2 = fma2(Kp[1][c], bc(Qu1), Kp[0][c] * bc(Qu0));
+    const f2 t3 = fma2(Qux[1][c], bc(kff[1]), Qux[0][c] * bc(kff[0]));
+    R.Vx[c] = ((Qxp[c] + t1) + t2) + t3;
+  }
+  // V_xx = Q_xx + K^T Q_uu K + K^T Q_ux + Q_xu K: row i, column pair c, one fma chain
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ci = i >> 1;
+    const float kq0 = (i & 1) ? KQ0[ci].y : KQ0[ci].x, kq1 = (i & 1) ? KQ1[ci].y : KQ1[ci].x;
+    const float k0i = (i & 1) ? Kp[0][ci].y : Kp[0][ci].x, k1i = (i & 1) ? Kp[1][ci].y : Kp[1][ci].x;
+    const float q0i = (i & 1) ? Qux[0][ci].y : Qux[0][ci].x, q1i = (i & 1) ? Qux[1][ci].y : Qux[1][ci].x;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f2 acc = fma2(bc(kq0), Kp[0][c], Q[i][c]);
+      acc = fma2(bc(kq1), Kp[1][c], acc);
+      acc = fma2(bc(k0i), Qux[0][c], acc);
+      acc = fma2(bc(k1i), Qux[1][c], acc);
+      acc = fma2(bc(q0i), Kp[0][c], acc);
+      R.V[i][c] = fma2(bc(q1i), Kp[1][c], acc);
+    }
+  }
+  return ok;
+}
+
 // backward pass (ilqr_backward, core/ddp.py:172-254)
 template <bool TRACK, int M>
 __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg, const Solve<TRACK>& S) {
@@ -535,6 +666,20 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     d1 = xn1 - c.t1;
     d2 = xn2 - c.t2;
   }
+#if DTMPC_FAST_RICPK
+  RicP R;
+  R.V[0][0] = f2{pxx[0], 0.f};
+  R.V[0][1] = f2{0.f, 0.f};
+  R.V[1][0] = f2{0.f, pxx[1]};
+  R.V[1][1] = f2{0.f, 0.f};
+  R.V[2][0] = f2{0.f, 0.f};
+  R.V[2][1] = f2{pxx[2], 0.f};
+  R.V[3][0] = f2{0.f, 0.f};
+  R.V[3][1] = f2{0.f, pxx[3]};
+  R.Vx[0] = f2{pxx[0] * d0, pxx[1] * d1};
+  R.Vx[1] = f2{pxx[2] * d2, pxx[3] * xnb};
+#define RVX(i) ((i) == 0 ? R.Vx[0].x : (i) == 1 ? R.Vx[0].y : (i) == 2 ? R.Vx[1].x : R.Vx[1].y)
+#else
   Riccati<float> R;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -544,9 +689,11 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
   R.Vx[1] = pxx[1] * d1;
   R.Vx[2] = pxx[2] * d2;
   R.Vx[3] = pxx[3] * xnb;
+#define RVX(i) (R.Vx[i])
+#endif
   float gxn, gyn;
   float dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
-  bool ok = finite(R.Vx[0]) && finite(R.Vx[1]) && finite(R.Vx[2]) && finite(R.Vx[3]);
+  bool ok = finite(RVX(0)) && finite(RVX(1)) && finite(RVX(2)) && finite(RVX(3));
   // step inputs one step ahead
   f4 nX = S.x(N - 1), nR = f4{0.f, 0.f, 0.f, 0.f};
   f2 nV = S.u(N - 1), nQ = f2{0.f, 0.f};
@@ -580,7 +727,11 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
       lu[1] = luu[1] * u1;
     }
     float Kk[8], kk[2];
+#if DTMPC_FAST_RICPK
+    ok = riccati_pk(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
+#else
     ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
+#endif
     S.G.store(S.r, k, Kk, kk);
     gxn = gxk;
     gyn = gyk;
@@ -600,7 +751,8 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     step(X, V, Rr, Q, k);
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) ok = ok && finite(R.Vx[i]);
+  for (int i = 0; i < 4; ++i) ok = ok && finite(RVX(i));
+#undef RVX
   return ok;
 }
 
