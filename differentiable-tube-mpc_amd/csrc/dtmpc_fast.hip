@@ -222,7 +222,45 @@ __device__ __forceinline__ f2 vexp2(f2 x) { return f2{__builtin_amdgcn_exp2f(x.x
 __device__ __forceinline__ f2 vexp(f2 x) { return pk_exp(x); }
 __device__ __forceinline__ float vlog(float x) { return m_log(x); }
 __device__ __forceinline__ f2 vlog(f2 x) { return pk_log(x); }
-__device__ __forceinline__ void vsincos(float x, float& s, float& c) { m_sincos(x, &s, &c); }
+// sin / cos for the forward passes: sincos_cw's Cody-Waite reduction x = r + j pi/2 and minimax
+// polynomials, with the quadrant applied WITHOUT selects: sin x = A s + B c, cos x = A c - B s with
+// (A, B) = (cos j pi/2, sin j pi/2) in {0, +-1} -- m = j - 4 floor((j + 1) / 4) in {-1, 0, 1, 2},
+// A = 1 - |m|, B = min(m, 2 - m).  Every product is by 0 or +-1, so the values are exactly the
+// quadrant-selected ones (the sign of a zero result aside); |x| > 65536 and non-finite take OCML.
+// Same operations element by element in the scalar (commit, start rollout, plant) and the pair (line
+// search) form: a committed tape is bitwise the candidate priced.
+#ifndef DTMPC_FAST_SINCOS_AB
+#define DTMPC_FAST_SINCOS_AB 1
+#endif
+__device__ __forceinline__ void sincos_poly(float r, float& s, float& c) {
+  const float z = r * r;
+  float ps = __builtin_fmaf(z, kSinS3, kSinS2);
+  ps = __builtin_fmaf(z, ps, kSinS1);
+  s = __builtin_fmaf(r * z, ps, r);
+  float pc = __builtin_fmaf(z, kCosK3, kCosK2);
+  pc = __builtin_fmaf(z, pc, kCosK1);
+  c = __builtin_fmaf(z * z, pc, __builtin_fmaf(-0.5f, z, 1.0f));
+}
+__device__ __forceinline__ void vsincos(float x, float& sn, float& cs) {
+#if DTMPC_FAST_SINCOS_AB
+  if (__builtin_expect(!(__builtin_fabsf(x) <= 65536.0f), 0)) {
+    sincosf(x, &sn, &cs);
+    return;
+  }
+  const float q = __builtin_rintf(x * k2oPi);
+  float r = __builtin_fmaf(-q, kPio2A, x);
+  r = __builtin_fmaf(-q, kPio2B, r);
+  r = __builtin_fmaf(-q, kPio2C, r);
+  float s, c;
+  sincos_poly(r, s, c);
+  const float m = __builtin_fmaf(-4.f, __builtin_floorf(__builtin_fmaf(q, 0.25f, 0.25f)), q);
+  const float A = 1.f - __builtin_fabsf(m), Bq = __builtin_fminf(m, 2.f - m);
+  sn = __builtin_fmaf(s, A, c * Bq);
+  cs = __builtin_fmaf(c, A, -(s * Bq));
+#else
+  m_sincos(x, &sn, &cs);
+#endif
+}
 __device__ __forceinline__ void vsincos(f2 x, f2& s, f2& c) { pk_sincos(x, s, c); }
 __device__ __forceinline__ bool vfinite(float x) { return finite(x); }
 __device__ __forceinline__ bool vfinite(f2 x) { return finite(x.x) && finite(x.y); }
@@ -799,6 +837,22 @@ __device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
       s[q] = __builtin_elementwise_fma(r[q] * z[q], ps, r[q]);
       c[q] = __builtin_elementwise_fma(z[q] * z[q], pc, __builtin_elementwise_fma(f2(-0.5f), z[q], f2(1.0f)));
     }
+#if DTMPC_FAST_SINCOS_AB
+    f2 A[NPR], Bq[NPR];
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      const f2 t = __builtin_elementwise_fma(qq[q], f2(0.25f), f2(0.25f));
+      const f2 m = __builtin_elementwise_fma(f2(-4.f), f2{__builtin_floorf(t.x), __builtin_floorf(t.y)}, qq[q]);
+      A[q] = f2{1.f - __builtin_fabsf(m.x), 1.f - __builtin_fabsf(m.y)};
+      const f2 w = f2(2.f) - m;
+      Bq[q] = f2{__builtin_fminf(m.x, w.x), __builtin_fminf(m.y, w.y)};
+    }
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      sn[q] = __builtin_elementwise_fma(s[q], A[q], c[q] * Bq[q]);
+      cs[q] = __builtin_elementwise_fma(c[q], A[q], -(s[q] * Bq[q]));
+    }
+#else
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
       const int j0 = (int)qq[q].x & 3, j1 = (int)qq[q].y & 3;
@@ -807,14 +861,15 @@ __device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
       sn[q] = f2{(j0 & 2) ? -so0 : so0, (j1 & 2) ? -so1 : so1};
       cs[q] = f2{((j0 + 1) & 2) ? -co0 : co0, ((j1 + 1) & 2) ? -co1 : co1};
     }
+#endif
     return;
   }
 #endif
 #pragma unroll
-  for (int q = 0; q < NPR; ++q) {
+  for (int q = 0; q < NPR; ++q) {  // some element out of range: each element as the scalar form
     float s0, c0, s1, c1;
-    m_sincos(x[q].x, &s0, &c0);
-    m_sincos(x[q].y, &s1, &c1);
+    vsincos(x[q].x, s0, c0);
+    vsincos(x[q].y, s1, c1);
     sn[q] = f2{s0, s1};
     cs[q] = f2{c0, c1};
   }

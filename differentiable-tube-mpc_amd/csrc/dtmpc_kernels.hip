@@ -230,16 +230,28 @@ struct TubeArgs {
 // trajectories) one lane per trajectory is exactly one wave per SIMD; two lanes (paired line search,
 // line_search_pair: each lane of a pair rolls out half the candidates, the rest of the step is
 // computed identically by both lanes and stored twice) measured 8.27 vs 7.54 ms there -- the
-// duplicated backward / commit work outweighs the overlap.  Below kPairBatch trajectories the machine
+// duplicated backward / commit work outweighs the overlap.  Below half the lane slots the machine
 // is mostly idle and the step is ONE wave's latency, which the paired line search cuts: there the
 // tube step uses two lanes.  DTMPC_TUBE_LANES=1|2 (environment) forces either, for the parity tests;
 // it is read by dtmpc_tube_lanes only, i.e. once, when the caller builds its state (state->lanes).
-constexpr int64_t kPairBatch = 16384;  // <= 512 paired waves: at most half a wave per SIMD
+// Two lanes while the paired waves still fit one per SIMD: 2 B <= (SIMDs x 64) lane slots of the
+// current device (MI355X: 256 CUs x 4 SIMDs x 64 = 65,536, i.e. B <= 32,768; measured at B = 32,768:
+// 3.63 ms paired vs 4.11 ms one lane, at B = 65,536 one lane wins).  Without a device (host-side
+// tests) the MI355X count is assumed.
+static int64_t lane_slots() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0) {
+    (void)hipGetLastError();
+    cus = 256;
+  }
+  return (int64_t)cus * 4 * 64;
+}
 
 static int tube_lanes_default(int64_t B) {
   const char* e = getenv("DTMPC_TUBE_LANES");
   if (e && (e[0] == '1' || e[0] == '2') && e[1] == 0) return e[0] - '0';
-  return B <= kPairBatch ? 2 : 1;
+  return 2 * B <= lane_slots() ? 2 : 1;
 }
 
 // One wave per SIMD is all either form gets (the two-lane form runs only at small batches), so the
