@@ -79,6 +79,7 @@ struct FArgs {
   int disturbance, write_log;
   unsigned long long seed;
   float wlo[3], whi[3];
+  int stagger;  // s_sleep(127) rounds before this workgroup starts (phase desynchronisation, see launch)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -163,11 +164,14 @@ __device__ __forceinline__ f4 rld4(Rsrc r, const RA& a, int k, unsigned off) {
 __device__ __forceinline__ f2 rld2(Rsrc r, const RA& a, int k, unsigned off) {
   return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, a.lo + off, a.so(k), 0));
 }
+#ifndef DTMPC_FAST_STPOL
+#define DTMPC_FAST_STPOL 0  // cache-policy bits of the record stores (A/B)
+#endif
 __device__ __forceinline__ void rst4(Rsrc r, const RA& a, int k, unsigned off, f4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, a.lo + off, a.so(k), 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, a.lo + off, a.so(k), DTMPC_FAST_STPOL);
 }
 __device__ __forceinline__ void rst2(Rsrc r, const RA& a, int k, unsigned off, f2 v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, a.lo + off, a.so(k), 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, a.lo + off, a.so(k), DTMPC_FAST_STPOL);
 }
 #else  // A/B: the same records through global loads / stores with a scalar row base
 __device__ __forceinline__ const char* kargs_ws();
@@ -1100,6 +1104,9 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
 #ifndef DTMPC_FAST_CM_DEPTH2
 #define DTMPC_FAST_CM_DEPTH2 1  // 0: one step of prefetch lead (measured 3 % slower)
 #endif
+#ifndef DTMPC_FAST_CM_LEAD
+#define DTMPC_FAST_CM_LEAD 2
+#endif
 // materialise the chosen candidate in place (commit_candidate): same arithmetic as its lane of the
 // line search; the old X[k+1] is read (prefetched) before it is overwritten
 template <bool TRACK, int M>
@@ -1128,26 +1135,30 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
     S.stx(k + 1, f4{s0, s1, s2, sb});
   };
 #if DTMPC_FAST_CM_DEPTH2
-  // four step buffers in rotation, each refilled two steps before it is used (the commit's step is
-  // short, ~250 instructions: one step of lead does not cover an HBM read).  A refill of step j reads
-  // the OLD X[j] before step j-1 overwrites it (issued earlier in program order).
+  // R = LEAD + 1 step buffers in rotation: each refilled LEAD steps before it is used (the commit's step
+  // is short, ~190 instructions, and a loaded chip stretches an HBM read past one or two of them).
+  // A refill of step j reads the OLD X[j] before step j-1 overwrites it (issued earlier in program
+  // order).  The loop is entered with the same outstanding vector-memory operations as its back edge
+  // carries (a refill and two stores per step): X row 0 is rewritten with x0 -- the value it holds --
+  // twice after each preload, so the wait-count state at the loop header is the same on both paths.
+  constexpr int LEAD = DTMPC_FAST_CM_LEAD, R = LEAD + 1;
   const int N1 = N - 1;
   auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
-  StepIn A, Bq, Cq, Dq;
-  load_step<false>(A, T0, 0);
-  load_step<false>(Bq, T0, ix(1));
-  for (int k = 0; k < N; k += 4) {
-    load_step<false>(Cq, T0, ix(k + 2));
-    step(A, k);
-    if (k + 1 >= N) break;
-    load_step<false>(Dq, T0, ix(k + 3));
-    step(Bq, k + 1);
-    if (k + 2 >= N) break;
-    load_step<false>(A, T0, ix(k + 4));
-    step(Cq, k + 2);
-    if (k + 3 >= N) break;
-    load_step<false>(Bq, T0, ix(k + 5));
-    step(Dq, k + 3);
+  const f4 X0v = f4{x0[0], x0[1], x0[2], x0[3]};
+  StepIn Bf[R];
+#pragma unroll
+  for (int j = 0; j < LEAD; ++j) {
+    load_step<false>(Bf[j], T0, ix(j));
+    rst2(S.r, S.XA, 0, 0, f2{X0v.x, X0v.y});
+    S.stx(0, X0v);
+  }
+  for (int k = 0; k < N; k += R) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      load_step<false>(Bf[(j + LEAD) % R], T0, ix(k + j + LEAD));
+      if (k + j >= N) break;
+      step(Bf[j], k + j);
+    }
   }
 #else
   StepIn cur, nxt;
@@ -1421,6 +1432,14 @@ tube_fast_kernel(FK kk) {
   const int t = P == 1 ? gl : (gl >> 1), h = P == 1 ? 0 : (gl & 1);  // t: index in the chunk
   const int i = i0 + t;                                                // index in the batch
   float acc[DTMPC_TUBE_SUMS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  {
+    // desynchronise the workgroups' phases: every wave runs the same sequence of passes, so without an
+    // offset the whole chip is in the same pass at once -- and the commit (the pass with the most
+    // bytes per instruction) then asks for about twice the HBM bandwidth while the line search leaves
+    // it idle.  Workgroup g starts (g mod 8) / 8 of `stagger` sleep rounds late.
+    const int n = kargs()->a.stagger * (int)(blockIdx.x & 7) / 8;
+    for (int r = 0; r < n; ++r) __builtin_amdgcn_s_sleep(127);
+  }
   Prof pf;
   pf.start();
   if (t < Bc) {
@@ -1699,6 +1718,10 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     a.whi[f] = float(cf->w_high[f]);
   }
   const int lanes = S->lanes;
+  {
+    const char* e = getenv("DTMPC_FAST_STAGGER");  // sleep rounds of ~8.1k cycles (A/B; default 0)
+    a.stagger = e ? atoi(e) : 0;
+  }
   // the batch in chunks whose workspace records fit one buffer resource (< 2^31 bytes), each chunk a
   // multiple of the workgroup size (its partial-sum rows follow the previous chunk's)
   const int64_t chunk = tube_fast_chunk(N);
