@@ -746,7 +746,7 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
   auto step = [&](const f4& X, const f2& V, const f4& Rr, const f2& Q, int k) {
     const float x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w, u0 = V.x, u1 = V.y;
     float sn, cs;
-    m_sincos(x2, &sn, &cs);
+    vsincos(x2, sn, cs);
     float gxk, gyk;
     const float dBk = dbarrier(p, h_grad<M>(p, x0, x1, gxk, gyk));
     const Jac<float> J = jac(p, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
@@ -1270,7 +1270,7 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const So
     const float x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w;
     const float u0 = V.x, u1 = V.y;
     float sn, cs;
-    m_sincos(x2, &sn, &cs);
+    vsincos(x2, sn, cs);
     float gxk, gyk;
     const float dBk = dbarrier(p, h_grad<M>(p, x0, x1, gxk, gyk));
     const Jac<float> J = jac(p, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
