@@ -1130,9 +1130,14 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
 #endif
     const float u0 = vclamp(cur.V0 + al * du0, p.umin0, p.umax0);
     const float u1 = vclamp(cur.V1 + al * du1, p.umin1, p.umax1);
+#ifdef DTMPC_FAST_DIAG_NOSTORE  // timing attribution only: the commit computes but stores nothing
+    fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
+    if (__builtin_isnan(s0 + u0 + u1)) S.stx(k + 1, f4{s0, s1, s2, sb});
+#else
     S.stu(k, f2{u0, u1});
     fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
     S.stx(k + 1, f4{s0, s1, s2, sb});
+#endif
   };
 #if DTMPC_FAST_CM_DEPTH2
   // R = LEAD + 1 step buffers in rotation: each refilled LEAD steps before it is used (the commit's step

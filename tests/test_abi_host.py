@@ -135,6 +135,14 @@ def test_arguments_validated_before_any_device_call(lib):
     rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
     assert rc == _abi.ERR_BAD_ARG and b"n_partials" in lib.dtmpc_last_error()
     assert lib.dtmpc_sensitivity_workspace_bytes(_abi.F64, 50, 10, 1) == 8 * 10 * (50 * 20 + 51 * 20)
+    # the fused episode reset validates before launching
+    rc = lib.dtmpc_tube_reset(_abi.F32, C.byref(spec), 8, None, C.byref(state), 1, 1, 1, None)
+    assert rc == _abi.ERR_BAD_ARG and b"NULL" in lib.dtmpc_last_error()
+    empty = _abi.DtmpcTubeState()
+    rc = lib.dtmpc_tube_reset(_abi.F32, C.byref(spec), 8, 1, C.byref(empty), 1, 1, 1, None)
+    assert rc == _abi.ERR_BAD_ARG and b"state" in lib.dtmpc_last_error()
+    rc = lib.dtmpc_tube_reset(_abi.F32, C.byref(spec), 0, 1, C.byref(state), 1, 1, 1, None)
+    assert rc == _abi.ERR_BAD_ARG
 
 
 def test_no_cpu_fallback():
