@@ -220,6 +220,21 @@ __device__ __forceinline__ float vclamp(float v, float lo, float hi) {
 }
 __device__ __forceinline__ f2 vclamp(f2 v, float lo, float hi) { return f2{vclamp(v.x, lo, hi), vclamp(v.y, lo, hi)}; }
 __device__ __forceinline__ float vmaxnan(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+// a * b + c of the forward passes: rounded twice (the reference's separate torch ops) by default; one
+// fused rounding with DTMPC_FAST_FWD_FMA (A/B).  Written at the same places of the line search, the
+// commit and the start rollout, so either way a committed tape is the candidate priced.
+#ifndef DTMPC_FAST_FWD_FMA
+#define DTMPC_FAST_FWD_FMA 0
+#endif
+template <class V>
+__device__ __forceinline__ V ffma(V a, V b, V c) {
+#if DTMPC_FAST_FWD_FMA
+  return __builtin_elementwise_fma(a, b, c);
+#else
+  DTMPC_NOCONTRACT
+  return a * b + c;
+#endif
+}
 __device__ __forceinline__ float vexp(float x) { return m_exp(x); }
 __device__ __forceinline__ float vexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ f2 vexp2(f2 x) { return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; }
@@ -312,7 +327,7 @@ __device__ __forceinline__ V h_sm(const FP& p, V px, V py) {
   for (int i = 0; i < M; ++i) {
     const V dx = px - p.cx[i];
     const V dy = py - p.cy[i];
-    hi[i] = dx * dx + dy * dy - p.r2[i];
+    hi[i] = ffma(dx, dx, dy * dy) - p.r2[i];
     hm = i == 0 ? hi[0] : vmin(hm, hi[i]);
   }
   const V zmax = p.neg_beta * hm;
@@ -359,11 +374,11 @@ __device__ __forceinline__ void fhat(const FP& p, V& x0, V& x1, V& x2, V& b, V u
   V sn, cs;
   vsincos(x2, sn, cs);
   const V dv = p.dt * u0;
-  x0 = x0 + dv * cs;
-  x1 = x1 + dv * sn;
-  x2 = x2 + p.dt * u1;
+  x0 = ffma(dv, cs, x0);
+  x1 = ffma(dv, sn, x1);
+  x2 = ffma(V(p.dt), u1, x2);
   const V Bn = vbarrier(p, h_sm<M>(p, x0, x1));
-  b = Bn - p.gamma * (Bc - b);
+  b = ffma(V(-p.gamma), Bc - b, Bn);
   Bc = Bn;
 }
 
@@ -392,9 +407,9 @@ __device__ __forceinline__ V stage(const FCost& c, V x0, V x1, V x2, V b, V u0, 
     e0 = u0;
     e1 = u1;
   }
-  const V sq = c.Q0 * d0 * d0 + c.Q1 * d1 * d1 + c.Q2 * d2 * d2;
-  const V sr = c.R0 * e0 * e0 + c.R1 * e1 * e1;
-  return sq + sr + c.qb * (b * b);
+  const V sq = ffma(c.Q2 * d2, d2, ffma(c.Q1 * d1, d1, (c.Q0 * d0) * d0));
+  const V sr = ffma(c.R1 * e1, e1, (c.R0 * e0) * e0);
+  return ffma(V(c.qb), b * b, sq + sr);
 }
 template <bool TRACK, class V>
 __device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, float r0, float r1, float r2) {
@@ -409,8 +424,8 @@ __device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, float r
     d1 = x1 - c.t1;
     d2 = x2 - c.t2;
   }
-  const V sq = c.Qf0 * d0 * d0 + c.Qf1 * d1 * d1 + c.Qf2 * d2 * d2;
-  return sq + c.qb * (b * b);
+  const V sq = ffma(c.Qf2 * d2, d2, ffma(c.Qf1 * d1, d1, (c.Qf0 * d0) * d0));
+  return ffma(V(c.qb), b * b, sq);
 }
 
 // K_row . e of the feedback du = k + K (x - X_k) (core/ddp.py:267-268), as an fma chain: the
@@ -894,8 +909,8 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
     const f2 du0 = s.kk.x + (s.Ka.x * e0 + s.Ka.y * e1 + s.Ka.z * e2 + s.Ka.w * e3);
     const f2 du1 = s.kk.y + (s.Kb.x * e0 + s.Kb.y * e1 + s.Kb.z * e2 + s.Kb.w * e3);
 #endif
-    u0[q] = s.V0 + C.al[q] * du0;
-    u1[q] = s.V1 + C.al[q] * du1;
+    u0[q] = ffma(C.al[q], du0, f2(s.V0));
+    u1[q] = ffma(C.al[q], du1, f2(s.V1));
   }
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
@@ -910,9 +925,9 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
     const f2 dv = p.dt * u0[q];
-    C.a0[q] = C.a0[q] + dv * cs[q];
-    C.a1[q] = C.a1[q] + dv * sn[q];
-    C.a2[q] = C.a2[q] + p.dt * u1[q];
+    C.a0[q] = ffma(dv, cs[q], C.a0[q]);
+    C.a1[q] = ffma(dv, sn[q], C.a1[q]);
+    C.a2[q] = ffma(f2(p.dt), u1[q], C.a2[q]);
   }
   // smooth-min h over the M obstacles (h_sm), all pairs together
   f2 hi[M][NPR], hm[NPR];
@@ -922,7 +937,7 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
     for (int q = 0; q < NPR; ++q) {
       const f2 dx = C.a0[q] - p.cx[i];
       const f2 dy = C.a1[q] - p.cy[i];
-      hi[i][q] = dx * dx + dy * dy - p.r2[i];
+      hi[i][q] = ffma(dx, dx, dy * dy) - p.r2[i];
       hm[q] = i == 0 ? hi[0][q] : vmin(hm[q], hi[i][q]);
     }
   f2 zmax[NPR], zl[NPR], se[NPR], z[NPR];
@@ -958,7 +973,7 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
   }
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
-    C.ab[q] = Bn[q] - p.gamma * (C.Bp[q] - C.ab[q]);
+    C.ab[q] = ffma(f2(-p.gamma), C.Bp[q] - C.ab[q], Bn[q]);
     C.Bp[q] = Bn[q];
   }
 }
@@ -1128,8 +1143,8 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
     const float du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
     const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
 #endif
-    const float u0 = vclamp(cur.V0 + al * du0, p.umin0, p.umax0);
-    const float u1 = vclamp(cur.V1 + al * du1, p.umin1, p.umax1);
+    const float u0 = vclamp(ffma(al, du0, cur.V0), p.umin0, p.umax0);
+    const float u1 = vclamp(ffma(al, du1, cur.V1), p.umin1, p.umax1);
 #ifdef DTMPC_FAST_DIAG_NOSTORE  // timing attribution only: the commit computes but stores nothing
     fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
     if (__builtin_isnan(s0 + u0 + u1)) S.stx(k + 1, f4{s0, s1, s2, sb});
