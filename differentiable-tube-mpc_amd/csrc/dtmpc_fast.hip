@@ -220,11 +220,13 @@ __device__ __forceinline__ float vclamp(float v, float lo, float hi) {
 }
 __device__ __forceinline__ f2 vclamp(f2 v, float lo, float hi) { return f2{vclamp(v.x, lo, hi), vclamp(v.y, lo, hi)}; }
 __device__ __forceinline__ float vmaxnan(float a, float b) { return __builtin_elementwise_maximum(a, b); }
-// a * b + c of the forward passes: rounded twice (the reference's separate torch ops) by default; one
-// fused rounding with DTMPC_FAST_FWD_FMA (A/B).  Written at the same places of the line search, the
-// commit and the start rollout, so either way a committed tape is the candidate priced.
+// a * b + c of the forward passes (dynamics, h_i, DBaS update, costs, the commit's u): one fused
+// rounding (v_fma / v_pk_fma; measured 4.66 -> 4.55 ms), the rounding of the oracle's FMA-contraction
+// build; DTMPC_FAST_FWD_FMA=0 rounds twice, as the reference's separate torch ops do.  Written at the
+// same places of the line search, the commit and the start rollout, so either way a committed tape is
+// the candidate priced.
 #ifndef DTMPC_FAST_FWD_FMA
-#define DTMPC_FAST_FWD_FMA 0
+#define DTMPC_FAST_FWD_FMA 1
 #endif
 template <class V>
 __device__ __forceinline__ V ffma(V a, V b, V c) {
@@ -466,14 +468,18 @@ struct StepIn {
   f2 kk;
 };
 
-template <bool TRACK>
+template <bool TRACK, bool LOADX = true>
 __device__ __forceinline__ void load_step(StepIn& L, const Solve<TRACK>& S, int k) {
-  const f4 X = S.x(k);
+  if (LOADX) {
+    const f4 X = S.x(k);
+    L.X0 = X.x;
+    L.X1 = X.y;
+    L.X2 = X.z;
+    L.X3 = X.w;
+  } else {
+    L.X0 = L.X1 = L.X2 = L.X3 = 0.f;
+  }
   const f2 V = S.u(k);
-  L.X0 = X.x;
-  L.X1 = X.y;
-  L.X2 = X.z;
-  L.X3 = X.w;
   L.V0 = V.x;
   L.V1 = V.y;
   L.Ka = rld4(S.r, S.G.K, k, 0);
@@ -1122,6 +1128,9 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
 #ifndef DTMPC_FAST_CM_LEAD
 #define DTMPC_FAST_CM_LEAD 2
 #endif
+#ifndef DTMPC_FAST_CM_RECOMP
+#define DTMPC_FAST_CM_RECOMP 0  // 1: the old tape's states are re-rolled from its controls, not read
+#endif
 // materialise the chosen candidate in place (commit_candidate): same arithmetic as its lane of the
 // line search; the old X[k+1] is read (prefetched) before it is overwritten
 template <bool TRACK, int M>
@@ -1129,13 +1138,26 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
   DTMPC_NOCONTRACT
   const int N = p.N;
   float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bc = Bc0;
+#if DTMPC_FAST_CM_RECOMP
+  // the tape's X is rollout(x0, U) by this same scalar fhat (init_tape, commit), so re-rolling the old
+  // controls reproduces the old X bit for bit and saves its 16 B per step of HBM reads
+  float o0 = s0, o1 = s1, o2 = s2, ob = sb, Bo = Bc0;
+  constexpr bool LX = false;
+#else
+  constexpr bool LX = true;
+#endif
   Solve<false> T0;  // no references needed
   T0.r = S.r;
   T0.XA = S.XA;
   T0.UA = S.UA;
   T0.G = S.G;
   auto step = [&](const StepIn& cur, int k) {
+#if DTMPC_FAST_CM_RECOMP
+    const float e0 = s0 - o0, e1 = s1 - o1, e2 = s2 - o2, e3 = sb - ob;
+    fhat<M>(p, o0, o1, o2, ob, cur.V0, cur.V1, Bo);
+#else
     const float e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
+#endif
 #if DTMPC_FAST_KFMA
     const float du0 = cur.kk.x + kdot(cur.Ka, e0, e1, e2, e3);
     const float du1 = cur.kk.y + kdot(cur.Kb, e0, e1, e2, e3);
@@ -1168,24 +1190,24 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
   StepIn Bf[R];
 #pragma unroll
   for (int j = 0; j < LEAD; ++j) {
-    load_step<false>(Bf[j], T0, ix(j));
+    load_step<false, LX>(Bf[j], T0, ix(j));
     rst2(S.r, S.XA, 0, 0, f2{X0v.x, X0v.y});
     S.stx(0, X0v);
   }
   for (int k = 0; k < N; k += R) {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      load_step<false>(Bf[(j + LEAD) % R], T0, ix(k + j + LEAD));
+      load_step<false, LX>(Bf[(j + LEAD) % R], T0, ix(k + j + LEAD));
       if (k + j >= N) break;
       step(Bf[j], k + j);
     }
   }
 #else
   StepIn cur, nxt;
-  load_step<false>(nxt, T0, 0);
+  load_step<false, LX>(nxt, T0, 0);
   for (int k = 0; k < N; ++k) {
     cur = nxt;
-    if (k + 1 < N) load_step<false>(nxt, T0, k + 1);
+    if (k + 1 < N) load_step<false, LX>(nxt, T0, k + 1);
     step(cur, k);
   }
 #endif

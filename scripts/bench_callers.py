@@ -71,4 +71,5 @@ steps = int(r.h_ran.sum())
 print(json.dumps({"path": "receding nominal MPC (run_nominal.py)", "batch": B, "H": a.H, "seconds": dt,
                   "solves": steps, "ilqr_solves_per_s": steps / dt, "ms_per_receding_step": dt * 1e3 / a.H,
                   "max_iter": icfg.max_iter, "line_search_alphas": len(icfg.line_search_alphas),
-                  "success": int((r.success_t >= 0).sum()), "collided": int(r.collided.sum())}), flush=True)
+                  "success": int((r.success_t >= 0).sum()), "collided": int(r.collided.sum()),
+                  "failed": int((r.status != 0).sum())}), flush=True)
