@@ -191,10 +191,19 @@ __device__ __forceinline__ void rst2(Rsrc, const RA& a, int k, unsigned off, f2 
 
 struct Gains {
   RA K, k;  // K and k records
+  // G0 (gamma = 0): K's column for the barrier state b is exactly zero (A's column 3 is (0, 0, 0, gamma),
+  // so Q_ux's is gamma * S = 0 and K = -Q_uu^-1 Q_ux keeps it), and the iLQR record is the 32 bytes
+  // K00 K01 K02 K10 | K11 K12 k0 k1 -- 8 B less per step, two loads instead of three
+  template <bool G0>
   __device__ __forceinline__ void store(Rsrc r, int s, const float* Kk, const float* kk) const {
-    rst4(r, K, s, 0, f4{Kk[0], Kk[1], Kk[2], Kk[3]});
-    rst4(r, K, s, 16, f4{Kk[4], Kk[5], Kk[6], Kk[7]});
-    rst2(r, k, s, 0, f2{kk[0], kk[1]});
+    if (G0) {
+      rst4(r, K, s, 0, f4{Kk[0], Kk[1], Kk[2], Kk[4]});
+      rst4(r, K, s, 16, f4{Kk[5], Kk[6], kk[0], kk[1]});
+    } else {
+      rst4(r, K, s, 0, f4{Kk[0], Kk[1], Kk[2], Kk[3]});
+      rst4(r, K, s, 16, f4{Kk[4], Kk[5], Kk[6], Kk[7]});
+      rst2(r, k, s, 0, f2{kk[0], kk[1]});
+    }
   }
 };
 
@@ -436,18 +445,19 @@ __device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, float r
 #ifndef DTMPC_FAST_KFMA
 #define DTMPC_FAST_KFMA 1
 #endif
-template <class V>
+template <bool G0, class V>
 __device__ __forceinline__ V kdot(const f4& K, V e0, V e1, V e2, V e3) {
   V t = K.x * e0;
   t = __builtin_elementwise_fma(V(K.y), e1, t);
   t = __builtin_elementwise_fma(V(K.z), e2, t);
-  return __builtin_elementwise_fma(V(K.w), e3, t);
+  return G0 ? t : __builtin_elementwise_fma(V(K.w), e3, t);  // G0: K.w = 0 (Gains)
 }
 
 // ---------------------------------------------------------------------------------------------
 // the tapes one iLQR solve works on
-template <bool TRACK>
+template <bool TRACK, bool G0 = false>
 struct Solve {
+  static constexpr bool g0 = G0;  // gamma = 0: the compact gain records (Gains)
   Rsrc r;         // the workspace
   RA XA, UA;      // this solve's tape records (states + barrier state, controls)
   RA XRA, URA;    // TRACK: the nominal plan's records
@@ -468,8 +478,8 @@ struct StepIn {
   f2 kk;
 };
 
-template <bool TRACK, bool LOADX = true>
-__device__ __forceinline__ void load_step(StepIn& L, const Solve<TRACK>& S, int k) {
+template <bool TRACK, bool LOADX = true, class SV>
+__device__ __forceinline__ void load_step(StepIn& L, const SV& S, int k) {
   if (LOADX) {
     const f4 X = S.x(k);
     L.X0 = X.x;
@@ -482,9 +492,16 @@ __device__ __forceinline__ void load_step(StepIn& L, const Solve<TRACK>& S, int 
   const f2 V = S.u(k);
   L.V0 = V.x;
   L.V1 = V.y;
-  L.Ka = rld4(S.r, S.G.K, k, 0);
-  L.Kb = rld4(S.r, S.G.K, k, 16);
-  L.kk = rld2(S.r, S.G.k, k, 0);
+  if (SV::g0) {
+    const f4 g0 = rld4(S.r, S.G.K, k, 0), g1 = rld4(S.r, S.G.K, k, 16);
+    L.Ka = f4{g0.x, g0.y, g0.z, 0.f};
+    L.Kb = f4{g0.w, g1.x, g1.y, 0.f};
+    L.kk = f2{g1.z, g1.w};
+  } else {
+    L.Ka = rld4(S.r, S.G.K, k, 0);
+    L.Kb = rld4(S.r, S.G.K, k, 16);
+    L.kk = rld2(S.r, S.G.k, k, 0);
+  }
   if (TRACK) {
     const f4 R = S.xr(k);
     const f2 Q = S.ur(k);
@@ -517,8 +534,8 @@ __device__ __forceinline__ void copy_out(int N, const Rsrc& r, const RA& XA, con
 
 // iLQR start (init_tape): V = clamp(V_init) (the warm start, ABI SoA), X = rollout(x0, V) into this
 // solve's records, and the alpha = 0 candidate's cost
-template <bool TRACK, int M>
-__device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const float* x0, const Solve<TRACK>& S,
+template <bool TRACK, int M, class SV>
+__device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const float* x0, const SV& S,
                                            bool want_cost) {
   DTMPC_NOCONTRACT
   const int N = p.N;
@@ -710,8 +727,8 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
 }
 
 // backward pass (ilqr_backward, core/ddp.py:172-254)
-template <bool TRACK, int M>
-__device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg, const Solve<TRACK>& S) {
+template <bool TRACK, int M, class SV>
+__device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg, const SV& S) {
   const int N = p.N;
   const float lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
   const float luu[2] = {2.f * c.R0, 2.f * c.R1};
@@ -795,7 +812,7 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
 #else
     ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
 #endif
-    S.G.store(S.r, k, Kk, kk);
+    S.G.template store<SV::g0>(S.r, k, Kk, kk);
     gxn = gxk;
     gyn = gyk;
     dBn = dBk;
@@ -901,7 +918,7 @@ __device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
 }
 
 // one step of the NPR pairs' rollouts: feedback + clamp, stage cost, DBaS-augmented Dubins move
-template <bool TRACK, int M, int NPR>
+template <bool TRACK, int M, int NPR, bool G0>
 __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepIn& s, Cand<NPR>& C) {
   DTMPC_NOCONTRACT
   f2 u0[NPR], u1[NPR];
@@ -909,8 +926,8 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
   for (int q = 0; q < NPR; ++q) {
     const f2 e0 = C.a0[q] - s.X0, e1 = C.a1[q] - s.X1, e2 = C.a2[q] - s.X2, e3 = C.ab[q] - s.X3;
 #if DTMPC_FAST_KFMA
-    const f2 du0 = s.kk.x + kdot(s.Ka, e0, e1, e2, e3);
-    const f2 du1 = s.kk.y + kdot(s.Kb, e0, e1, e2, e3);
+    const f2 du0 = s.kk.x + kdot<G0>(s.Ka, e0, e1, e2, e3);
+    const f2 du1 = s.kk.y + kdot<G0>(s.Kb, e0, e1, e2, e3);
 #else
     const f2 du0 = s.kk.x + (s.Ka.x * e0 + s.Ka.y * e1 + s.Ka.z * e2 + s.Ka.w * e3);
     const f2 du1 = s.kk.y + (s.Kb.x * e0 + s.Kb.y * e1 + s.Kb.z * e2 + s.Kb.w * e3);
@@ -987,9 +1004,9 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
 // Returns the chosen original position (or -1 if any candidate or Jprev is non-finite), its cost
 // and alpha.  P = 1: the six candidates as three pairs; P = 2: three per lane (two pairs, the last
 // one doubled), the pair of lanes combining their minima by one DPP swap.
-template <bool TRACK, int M, int P>
+template <bool TRACK, int M, int P, class SV>
 __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FIlqr& cf, const float* x0, float Bc0,
-                                           const Solve<TRACK>& S, float Jprev, int h, float& bestJ, float& al_out) {
+                                           const SV& S, float Jprev, int h, float& bestJ, float& al_out) {
   DTMPC_NOCONTRACT
   constexpr int NL = NC / P;          // candidates of this lane
   constexpr int NPR = (NL + 1) / 2;   // pairs
@@ -1019,26 +1036,26 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   load_step<TRACK>(Bs, S, ix(1));
   for (int k = 0; k < N; k += 4) {
     load_step<TRACK>(Cs, S, ix(k + 2));
-    ls_step<TRACK, M, NPR>(p, c, A, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, A, C);
     if (k + 1 >= N) break;
     load_step<TRACK>(Ds, S, ix(k + 3));
-    ls_step<TRACK, M, NPR>(p, c, Bs, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, Bs, C);
     if (k + 2 >= N) break;
     load_step<TRACK>(A, S, ix(k + 4));
-    ls_step<TRACK, M, NPR>(p, c, Cs, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, Cs, C);
     if (k + 3 >= N) break;
     load_step<TRACK>(Bs, S, ix(k + 5));
-    ls_step<TRACK, M, NPR>(p, c, Ds, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, Ds, C);
   }
   } else {
   StepIn A, Bs;
   load_step<TRACK>(A, S, 0);
   load_step<TRACK>(Bs, S, N1 < 1 ? N1 : 1);
   for (int k = 0; k < N; k += 2) {
-    ls_step<TRACK, M, NPR>(p, c, A, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, A, C);
     load_step<TRACK>(A, S, uidx(k + 2 < N1 ? k + 2 : N1));
     if (k + 1 < N) {
-      ls_step<TRACK, M, NPR>(p, c, Bs, C);
+      ls_step<TRACK, M, NPR, SV::g0>(p, c, Bs, C);
       load_step<TRACK>(Bs, S, uidx(k + 3 < N1 ? k + 3 : N1));
     }
   }
@@ -1133,8 +1150,8 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
 #endif
 // materialise the chosen candidate in place (commit_candidate): same arithmetic as its lane of the
 // line search; the old X[k+1] is read (prefetched) before it is overwritten
-template <bool TRACK, int M>
-__device__ __forceinline__ void commit(const FP& p, float al, const float* x0, float Bc0, const Solve<TRACK>& S) {
+template <bool TRACK, int M, class SV>
+__device__ __forceinline__ void commit(const FP& p, float al, const float* x0, float Bc0, const SV& S) {
   DTMPC_NOCONTRACT
   const int N = p.N;
   float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bc = Bc0;
@@ -1146,7 +1163,7 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
 #else
   constexpr bool LX = true;
 #endif
-  Solve<false> T0;  // no references needed
+  Solve<false, SV::g0> T0;  // no references needed
   T0.r = S.r;
   T0.XA = S.XA;
   T0.UA = S.UA;
@@ -1159,8 +1176,8 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
     const float e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
 #endif
 #if DTMPC_FAST_KFMA
-    const float du0 = cur.kk.x + kdot(cur.Ka, e0, e1, e2, e3);
-    const float du1 = cur.kk.y + kdot(cur.Kb, e0, e1, e2, e3);
+    const float du0 = cur.kk.x + kdot<SV::g0>(cur.Ka, e0, e1, e2, e3);
+    const float du1 = cur.kk.y + kdot<SV::g0>(cur.Kb, e0, e1, e2, e3);
 #else
     const float du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
     const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
@@ -1238,9 +1255,9 @@ __device__ __forceinline__ void ls_stat(int trk, int best, float al, const FIlqr
 #endif
 
 // iLQR for one trajectory (ilqr_traj, core/ddp.py:102-307)
-template <bool TRACK, int M, int P>
+template <bool TRACK, int M, int P, class SV>
 __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const float* x0,
-                                    const Solve<TRACK>& S, int h, int& iters, Prof& pf) {
+                                    const SV& S, int h, int& iters, Prof& pf) {
   constexpr int ph = TRACK ? 4 : 0;  // phase-timer slots (profiling builds)
   float Jcur = init_tape<TRACK, M>(p, c, x0, S, cf.zpos >= 0 && cf.max_iter > 0);
   const float Bc0 = barrier_at<M>(p, x0[0], x0[1]);
@@ -1280,8 +1297,8 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
 // ---------------------------------------------------------------------------------------------
 // DDP sensitivity with the paper upper loss + DOC gradient (sens_traj<float, false, false, true>,
 // core/ddp.py:317-427, core/tube_mpc.py:915-976): acc = L, gQ(3), gR(2), gqb
-template <int M>
-__device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const Solve<true>& S, const RA& A8, const RA& A2,
+template <int M, class SV>
+__device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV& S, const RA& A8, const RA& A2,
                                            float* acc) {
   const int N = p.N;
   const float lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
@@ -1353,7 +1370,7 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const So
 #pragma unroll
       for (int j = 0; j < 4; ++j) R.Vxx[i][j] = Qxx[i][j] + (Qxu[i][0] * Kk[j] + Qxu[i][1] * Kk[4 + j]);
     }
-    S.G.store(S.r, k, Kk, kk);
+    S.G.template store<false>(S.r, k, Kk, kk);  // full records: its own K and k
     rst4(S.r, A8, k, 0, f4{J.a02, J.a12, J.a30, J.a31});
     rst4(S.r, A8, k, 16, f4{J.a32, J.b00, J.b10, J.b30});
     rst2(S.r, A2, k, 0, f2{J.b31, float((act0 ? 1 : 0) + (act1 ? 2 : 0))});
@@ -1464,7 +1481,7 @@ __device__ __forceinline__ FP phase_p() {
   return p;
 }
 
-template <int M, int P>
+template <int M, int P, bool G0>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P, P)))
 tube_fast_kernel(FK kk) {
   (void)kk;  // read through kargs()
@@ -1505,7 +1522,7 @@ tube_fast_kernel(FK kk) {
     }
     {  // nominal MPC (fixed weights, :813-857)
       KArg* K = kargs();
-      Solve<false> Sn;
+      Solve<false, G0> Sn;
       Sn.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
       Sn.XA = RA{K->a.oXn, cb * 16u, l16};
       Sn.UA = RA{K->a.oUn, cb * 8u, l8};
@@ -1532,7 +1549,7 @@ tube_fast_kernel(FK kk) {
       ca.qb = th[5];
       ca.t0 = ca.t1 = ca.t2 = 0.f;
     }
-    Solve<true> Sa;
+    Solve<true, G0> Sa;
     {  // ancillary MPC tracking the nominal plan (:863-909)
       KArg* K = kargs();
       Sa.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
@@ -1760,6 +1777,10 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     a.whi[f] = float(cf->w_high[f]);
   }
   const int lanes = S->lanes;
+  // gamma = 0 (the paper's DBaS): the compact gain records (fk::Gains); DTMPC_FAST_G0=0 (environment,
+  // read at each call) keeps the general records, for the tests that compare both
+  bool g0 = p.gamma == 0.f;
+  if (const char* e = getenv("DTMPC_FAST_G0")) g0 = g0 && !(e[0] == '0' && e[1] == 0);
   {
     const char* e = getenv("DTMPC_FAST_STAGGER");  // sleep rounds of ~8.1k cycles (A/B; default 0)
     a.stagger = e ? atoi(e) : 0;
@@ -1782,12 +1803,14 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     a.oA2 = 2 * X + 3 * U + 2 * K;
     a.wsz = 2 * X + 4 * U + 2 * K;
     const dim3 grid = grid_for(Bc * lanes);
+#define FAST_LAUNCH(m, l, g) hipLaunchKernelGGL((fk::tube_fast_kernel<m, l, g>), grid, dim3(kBlock), 0, st, kk)
 #define FAST_CASE(m)                                                                                       \
   case m:                                                                                                  \
-    if (lanes == 2)                                                                                        \
-      hipLaunchKernelGGL((fk::tube_fast_kernel<m, 2>), grid, dim3(kBlock), 0, st, kk);                   \
-    else                                                                                                   \
-      hipLaunchKernelGGL((fk::tube_fast_kernel<m, 1>), grid, dim3(kBlock), 0, st, kk);                   \
+    if (lanes == 2) {                                                                                      \
+      if (g0) FAST_LAUNCH(m, 2, true); else FAST_LAUNCH(m, 2, false);                                      \
+    } else {                                                                                               \
+      if (g0) FAST_LAUNCH(m, 1, true); else FAST_LAUNCH(m, 1, false);                                      \
+    }                                                                                                      \
     break;
     switch (sp->n_obstacles) {
 #ifdef DTMPC_FAST_M_ONLY
@@ -1798,6 +1821,7 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
       default: return set_err(DTMPC_ERR_BAD_ARG, "fast tube step: obstacle count not instantiated");
     }
 #undef FAST_CASE
+#undef FAST_LAUNCH
   }
   return check_launch("tube_fast_kernel");
 }

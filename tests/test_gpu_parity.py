@@ -621,6 +621,40 @@ def test_tube_step_fast_chunked_bitwise(dev, lanes, monkeypatch):
         assert torch.equal(runs[0][k], runs[1][k]), k
 
 
+@pytest.mark.parametrize("lanes", ["1", "2"])
+def test_tube_step_fast_gamma0_records(dev, lanes, monkeypatch):
+    """gamma = 0 (the paper's DBaS) makes the column of K for the barrier state exactly zero, and the
+    fast kernel then keeps K and k in one 32-byte record per step (dtmpc_fast.hip fk::Gains).  The
+    general 40-byte records (DTMPC_FAST_G0=0) must give the same values -- an exact zero term dropped
+    from the feedback sum changes nothing but, at most, the sign of a zero -- over two closed-loop
+    steps: states, tapes, log rows, partial sums and the shared theta."""
+    import dataclasses
+
+    from diff_tube_mpc_strict_pt.core import TubeMPC
+
+    monkeypatch.setenv("DTMPC_TUBE_LANES", lanes)
+    st = paper_setup()
+    assert st.problem.dbas_gamma == 0.0
+    st = dataclasses.replace(st, ilqr_nom=dataclasses.replace(st.ilqr_nom, tol=-1.0),
+                             ilqr_aux=dataclasses.replace(st.ilqr_aux, tol=-1.0))
+    B = 700
+    rng = np.random.default_rng(6)
+    x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(np.float32)
+    names = ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux", "theta", "status", "log", "partials")
+    runs = []
+    for g0 in ("1", "0"):
+        monkeypatch.setenv("DTMPC_FAST_G0", g0)
+        m = TubeMPC(st, batch=B, device=dev, dtype=torch.float32, disturbance="philox", seed=4, write_log=True)
+        m.reset(_t(x, torch.float32, dev))
+        m.step()
+        m.step()
+        torch.cuda.synchronize()
+        runs.append({k: getattr(m, k).clone() for k in names if getattr(m, k, None) is not None})
+    assert (runs[0]["status"] == 0).all()
+    for k in runs[0]:
+        assert torch.equal(runs[0][k], runs[1][k]), k
+
+
 @pytest.mark.parametrize("tag", ["f64", "f32"])
 def test_status_and_errors(dev, tag):
     """Non-finite inputs raise FloatingPointError (core/ddp.py:138-159); bad arguments ValueError."""
