@@ -148,6 +148,7 @@ __device__ __forceinline__ void st2(float* q, f2 v) { *(f2*)__builtin_assume_ali
 // and 48-byte gain records).
 //   X   [N+1][Bc][4]  x0 x1 x2 b        U  [N][Bc][2]  u0 u1      (nominal and ancillary tapes)
 //   K   [N][Bc][8]    K00..K03 K10..K13 k  [N][Bc][2]  k0 k1      (gains)
+//                     gamma = 0 (Gains<G0>): K [N][Bc][8] = K00 K01 K02 K10 K11 K12 k0 k1, k unused
 //   A8  [N][Bc][8]    a02 a12 a30 a31 a32 b00 b10 b30   A2 [N][Bc][2] b31 act  (sensitivity scratch)
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
