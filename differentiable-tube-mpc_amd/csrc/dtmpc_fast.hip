@@ -516,7 +516,9 @@ __device__ __forceinline__ void load_step(StepIn& L, const SV& S, int k) {
   }
 }
 
-// the solved tape out to the ABI SoA arrays (X, U), once per solve
+// the solved tape out to the ABI SoA arrays, once per solve: X as solved, U as the next step's warm
+// start -- the tube step's shift V <- [V[1:], V[-1]] (core/tube_mpc.py:1015-1020) applied on the way
+// out (the step's plant and log read the plan's first controls from the records)
 __device__ __forceinline__ void copy_out(int N, const Rsrc& r, const RA& XA, const RA& UA, const Soa<4>& X,
                                          const Soa<2>& U) {
   for (int k = 0; k <= N; ++k) {
@@ -527,8 +529,14 @@ __device__ __forceinline__ void copy_out(int N, const Rsrc& r, const RA& XA, con
     X.st(k, 3, x.w);
     if (k < N) {
       const f2 u = rld2(r, UA, k, 0);
-      U.st(k, 0, u.x);
-      U.st(k, 1, u.y);
+      if (k > 0) {
+        U.st(k - 1, 0, u.x);
+        U.st(k - 1, 1, u.y);
+      }
+      if (k == N - 1) {
+        U.st(k, 0, u.x);
+        U.st(k, 1, u.y);
+      }
     }
   }
 }
@@ -1579,9 +1587,10 @@ tube_fast_kernel(FK kk) {
       KArg* K = kargs();
       const FArgs& a = K->a;
       const FP p = phase_p<M>();
-      const Soa<2> Un{(char*)a.Unom, 2u * bb, L}, Ua{(char*)a.Uaux, 2u * bb, L};
-      const float u0 = Ua.ld(0, 0), u1 = Ua.ld(0, 1);
-      const float v0 = Un.ld(0, 0), v1 = Un.ld(0, 1);
+      // the plans' first controls, from the records (the ABI tapes already hold the shifted warm starts)
+      const f2 ua = rld2(Sa.r, Sa.UA, 0, 0), un = rld2(Sa.r, RA{a.oUn, cb * 8u, l8}, 0, 0);
+      const float u0 = ua.x, u1 = ua.y;
+      const float v0 = un.x, v1 = un.y;
       float w[3];
       if (a.disturbance == 0) {
         w[0] = a.w[i];
@@ -1627,13 +1636,6 @@ tube_fast_kernel(FK kk) {
         a.xbar[nb + i] = q1;
         a.xbar[2 * nb + i] = q2;
         a.bbar[i] = qb;
-      }
-      // warm-start shift V <- [V[1:], V[-1]]  (:1015-1020)
-      for (int k = 0; k + 1 < p.N; ++k) {
-        Un.st(k, 0, Un.ld(k + 1, 0));
-        Un.st(k, 1, Un.ld(k + 1, 1));
-        Ua.st(k, 0, Ua.ld(k + 1, 0));
-        Ua.st(k, 1, Ua.ld(k + 1, 1));
       }
       acc[7] = 1.f;
       if (st || h != 0) {  // healthy trajectories only; a lane pair counts once
