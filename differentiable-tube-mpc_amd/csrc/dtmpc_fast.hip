@@ -519,23 +519,41 @@ __device__ __forceinline__ void load_step(StepIn& L, const SV& S, int k) {
 // the solved tape out to the ABI SoA arrays, once per solve: X as solved, U as the next step's warm
 // start -- the tube step's shift V <- [V[1:], V[-1]] (core/tube_mpc.py:1015-1020) applied on the way
 // out (the step's plant and log read the plan's first controls from the records)
+// Rows are read two ahead of their stores (a load waited for right before its own stores would leave
+// one memory latency per row exposed).
 __device__ __forceinline__ void copy_out(int N, const Rsrc& r, const RA& XA, const RA& UA, const Soa<4>& X,
                                          const Soa<2>& U) {
-  for (int k = 0; k <= N; ++k) {
-    const f4 x = rld4(r, XA, k, 0);
-    X.st(k, 0, x.x);
-    X.st(k, 1, x.y);
-    X.st(k, 2, x.z);
-    X.st(k, 3, x.w);
-    if (k < N) {
-      const f2 u = rld2(r, UA, k, 0);
-      if (k > 0) {
-        U.st(k - 1, 0, u.x);
-        U.st(k - 1, 1, u.y);
-      }
-      if (k == N - 1) {
-        U.st(k, 0, u.x);
-        U.st(k, 1, u.y);
+  const int N1 = N - 1;
+  auto iu = [&](int j) { return uidx(j < N1 ? j : N1); };
+  auto ix = [&](int j) { return uidx(j < N ? j : N); };
+  f4 xq[3];
+  f2 uq[3];
+  xq[0] = rld4(r, XA, 0, 0);
+  uq[0] = rld2(r, UA, 0, 0);
+  xq[1] = rld4(r, XA, ix(1), 0);
+  uq[1] = rld2(r, UA, iu(1), 0);
+  for (int k = 0; k <= N; k += 3) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int kk = k + j;
+      xq[(j + 2) % 3] = rld4(r, XA, ix(kk + 2), 0);
+      uq[(j + 2) % 3] = rld2(r, UA, iu(kk + 2), 0);
+      if (kk > N) break;
+      const f4 x = xq[j];
+      X.st(kk, 0, x.x);
+      X.st(kk, 1, x.y);
+      X.st(kk, 2, x.z);
+      X.st(kk, 3, x.w);
+      if (kk < N) {
+        const f2 u = uq[j];
+        if (kk > 0) {
+          U.st(kk - 1, 0, u.x);
+          U.st(kk - 1, 1, u.y);
+        }
+        if (kk == N1) {
+          U.st(kk, 0, u.x);
+          U.st(kk, 1, u.y);
+        }
       }
     }
   }
@@ -1332,9 +1350,18 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV
     const f4 XN = S.x(N);
     dBn = dbarrier(p, h_grad<M>(p, XN.x, XN.y, gxn, gyn));
   }
+  // step inputs read one step ahead (the loop's record stores would otherwise sit between a step's
+  // loads and their use, exposing one memory latency per step)
+  f4 nX = S.x(N - 1), nR = S.xr(N - 1);
+  f2 nV = S.u(N - 1);
   for (int k = N - 1; k >= 0; --k) {
-    const f4 X = S.x(k), Rr = S.xr(k);
-    const f2 V = S.u(k);
+    const f4 X = nX, Rr = nR;
+    const f2 V = nV;
+    if (k > 0) {
+      nX = S.x(k - 1);
+      nR = S.xr(k - 1);
+      nV = S.u(k - 1);
+    }
     const float x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w;
     const float u0 = V.x, u1 = V.y;
     float sn, cs;
@@ -1388,18 +1415,36 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV
   float d[4] = {0.f, 0.f, 0.f, 0.f};
   float L1 = 0.f, L2 = 0.f, gQ0 = 0.f, gQ1 = 0.f, gQ2 = 0.f, gR0 = 0.f, gR1 = 0.f, gqb = 0.f;
   const float g = p.gamma, dt = p.dt;
+  struct FwdIn {
+    f4 Ka, Kb, A0, A1, X, Rr;
+    f2 kf, A2r, V, Q;
+  };
+  auto fload = [&](FwdIn& F, int k) {
+    F.Ka = rld4(S.r, S.G.K, k, 0);
+    F.Kb = rld4(S.r, S.G.K, k, 16);
+    F.kf = rld2(S.r, S.G.k, k, 0);
+    F.A0 = rld4(S.r, A8, k, 0);
+    F.A1 = rld4(S.r, A8, k, 16);
+    F.A2r = rld2(S.r, A2, k, 0);
+    F.X = S.x(k);
+    F.Rr = S.xr(k);
+    F.V = S.u(k);
+    F.Q = S.ur(k);
+  };
+  FwdIn Fn;
+  fload(Fn, 0);
   for (int k = 0; k < N; ++k) {
-    const f4 Ka = rld4(S.r, S.G.K, k, 0), Kb = rld4(S.r, S.G.K, k, 16);
-    const f2 kf = rld2(S.r, S.G.k, k, 0);
-    const f4 A0 = rld4(S.r, A8, k, 0), A1 = rld4(S.r, A8, k, 16);
-    const f2 A2r = rld2(S.r, A2, k, 0);
+    const FwdIn F = Fn;
+    if (k + 1 < N) fload(Fn, k + 1);
+    const f4 Ka = F.Ka, Kb = F.Kb, A0 = F.A0, A1 = F.A1;
+    const f2 kf = F.kf, A2r = F.A2r;
     const float a02 = A0.x, a12 = A0.y, a30 = A0.z, a31 = A0.w, a32 = A1.x, b00 = A1.y, b10 = A1.z, b30 = A1.w,
                 b31 = A2r.x;
     const int act = (int)A2r.y;
     const float v0 = (act & 1) ? 0.f : kf.x + (Ka.x * d[0] + Ka.y * d[1] + Ka.z * d[2] + Ka.w * d[3]);
     const float v1 = (act & 2) ? 0.f : kf.y + (Kb.x * d[0] + Kb.y * d[1] + Kb.z * d[2] + Kb.w * d[3]);
-    const f4 X = S.x(k), Rr = S.xr(k);
-    const f2 V = S.u(k), Q = S.ur(k);
+    const f4 X = F.X, Rr = F.Rr;
+    const f2 V = F.V, Q = F.Q;
     const float e0 = X.x - Rr.x;
     const float e1 = X.y - Rr.y;
     const float e2 = X.z - Rr.z;
