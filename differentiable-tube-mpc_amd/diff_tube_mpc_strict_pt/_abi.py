@@ -173,6 +173,11 @@ PROTOTYPES = {
     "dtmpc_dbas_rollout": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), I64, P, P, P, P]),
     "dtmpc_dbas_init": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), I64, P, P, P]),
     "dtmpc_linearize": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), I64, P, P, P, P, P, P, P, P, P]),
+    # include/dtmpc_control.h
+    "dtmpc_tanh_cost_derivs": (
+        C.c_int,
+        [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), I64, P, P, P, P, P, P, P, P, P, P],
+    ),
     "dtmpc_ilqr_solve": (
         C.c_int,
         [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, P, P, P, P, P, P, P, P, P, P],

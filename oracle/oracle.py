@@ -132,6 +132,20 @@ class Oracle:
                                     _p(A), _p(Bm), _p(lx), _p(lu))
         return aos(A).reshape(B, N, 4, 4), aos(Bm).reshape(B, N, 4, 2), aos(lx), aos(lu)
 
+    def tanh_cost_derivs(self, spec, cost, X, Vd, Xref=None, Uref=None):
+        """u(v), du/dv and the v-space stage-cost derivatives (l_x, l_v, diag l_vv) of the tanh-box
+        control along a tape (oracle_tanh_cost_derivs: core/control.py:10-35, core/cost_derivs.py:16-107)."""
+        X = self._a(X)
+        B, N = X.shape[0], spec.horizon
+        Xs, Vs = soa(X), soa(self._a(Vd))
+        Xr = soa(self._a(Xref)[..., :3]) if Xref is not None else None
+        Ur = soa(self._a(Uref)) if Uref is not None else None
+        U, dU, lv, lvv = (np.empty((N, 2, B), self.dt) for _ in range(4))
+        lx = np.empty((N, 4, B), self.dt)
+        self._f("oracle_tanh_cost_derivs")(C.byref(spec), C.byref(cost), C.c_longlong(B), _p(Xs), _p(Vs), _p(Xr), _p(Ur),
+                                           _p(U), _p(dU), _p(lx), _p(lv), _p(lvv))
+        return {"u": aos(U), "dudv": aos(dU), "lx": aos(lx), "lv": aos(lv), "lvv": aos(lvv)}
+
     def ilqr_solve(self, spec, cost, cfg, x0, V_init, Xref=None, Uref=None):
         x0 = self._a(x0)
         B, N = x0.shape[0], spec.horizon

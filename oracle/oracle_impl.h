@@ -1115,5 +1115,52 @@ void FN(oracle_theta_update)(const dtmpc_adapt_cfg* cfg, double inv_batch, const
 
 #include "oracle_general.h"
 
+/* Tanh-box control map and stage-cost derivatives in the decision variable v, along a tape.
+ *   u(v)      = u_min + (u_max - u_min) * (tanh(v) + 1) * 0.5     core/control.py:22-27
+ *   du/dv     = ((u_max - u_min) * 0.5) * (1 - tanh(v)^2)         core/control.py:29-35
+ *   d2u/dv2   = scale * ((-2 tanh(v)) * sech2)                    core/cost_derivs.py:16-24
+ *   nominal   l_x = [2Q dx, 2qb b], l_v = 2R u du/dv,             core/cost_derivs.py:27-55
+ *             l_vv = 2R (du/dv^2 + u d2u/dv2)   (dx = x - target)
+ *   auxiliary the same with u - u_ref in place of u, dx = x - x_ref  core/cost_derivs.py:79-107
+ * (l_xx = diag(2Q, 2qb) and l_vx = 0 are constants of the cost.)  Each product is rounded in the
+ * order torch evaluates the reference's expression.  SoA in/out; any output may be NULL. */
+void FN(oracle_tanh_cost_derivs)(const dtmpc_spec* sp, const dtmpc_cost* cp, long long B, const REAL* X,
+                                 const REAL* Vd, const REAL* Xref, const REAL* Uref, REAL* U, REAL* dU,
+                                 REAL* lx, REAL* lv, REAL* lvv) {
+  SPEC_T s;
+  COST_T c;
+  FN(spec_from)(sp, &s);
+  FN(cost_from)(cp, &c);
+  const int N = s.N;
+  const int trk = c.kind == DTMPC_COST_TRACK;
+  for (long long i = 0; i < B; ++i)
+    for (int k = 0; k < N; ++k) {
+      REAL xh[4], dx[3];
+      for (int f = 0; f < 4; ++f) xh[f] = X[((long long)k * 4 + f) * B + i];
+      for (int f = 0; f < 3; ++f)
+        dx[f] = xh[f] - (trk ? Xref[((long long)k * 3 + f) * B + i] : c.target[f]);
+      for (int f = 0; f < 3; ++f)
+        if (lx) lx[((long long)k * 4 + f) * B + i] = ((REAL)2 * c.Q[f]) * dx[f];
+      if (lx) lx[((long long)k * 4 + 3) * B + i] = ((REAL)2 * c.qb) * xh[3];
+      for (int a = 0; a < 2; ++a) {
+        const long long o = ((long long)k * 2 + a) * B + i;
+        const REAL v = Vd[o];
+        const REAL th = M_TANH(v);
+        const REAL w = s.umax[a] - s.umin[a];
+        const REAL u = s.umin[a] + (w * (th + (REAL)1)) * (REAL)0.5;
+        const REAL scale = w * (REAL)0.5;
+        const REAL sech2 = (REAL)1 - th * th;
+        const REAL du_dv = scale * sech2;
+        const REAL d2u = scale * (((REAL)-2 * th) * sech2);
+        const REAL e = trk ? u - Uref[o] : u;
+        const REAL r2 = (REAL)2 * c.R[a];
+        if (U) U[o] = u;
+        if (dU) dU[o] = du_dv;
+        if (lv) lv[o] = (r2 * e) * du_dv;
+        if (lvv) lvv[o] = r2 * (du_dv * du_dv + e * d2u);
+      }
+    }
+}
+
 #undef SPEC_T
 #undef COST_T

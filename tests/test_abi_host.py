@@ -4,6 +4,7 @@ before any device call, and the config -> typed-problem mapping follows the refe
 from __future__ import annotations
 
 import ctypes as C
+import glob
 import math
 import os
 import re
@@ -16,10 +17,12 @@ from _common import config
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "dtmpc.h")
+HEADERS = sorted(glob.glob(os.path.join(REPO, "include", "*.h")))
 
 
 def header_functions() -> set:
-    src = open(HEADER).read()
+    """Every dtmpc_* function declared in include/*.h."""
+    src = "\n".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return set(re.findall(r"^\s*(?:const\s+)?[\w]+[\s\*]+(dtmpc_\w+)\s*\(", src, flags=re.M))
 
