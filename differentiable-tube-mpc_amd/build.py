@@ -3,7 +3,7 @@
 Plain hipcc, no build system: the translation units compiled in parallel, then linked --
 csrc/dtmpc_kernels.hip (paper path + per-function entry points), csrc/dtmpc_general.hip (general IFT
 path), csrc/dtmpc_receding.hip (receding-horizon nominal MPC driver), csrc/dtmpc_control.hip (tanh-box
-control map + cost derivatives).
+control map + cost derivatives), csrc/dtmpc_ocp.hip (tape cost of core/ocp.py).
 """
 from __future__ import annotations
 
@@ -16,7 +16,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f)
         for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_general.hip", "dtmpc_receding.hip",
-                  "dtmpc_control.hip")]
+                  "dtmpc_control.hip", "dtmpc_ocp.hip")]
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solver.hpp", "dtmpc_general.hpp",
                                                  "dtmpc_host.hpp", "dtmpc_ls_pk.hpp")] + [
     os.path.join(os.path.dirname(HERE), "include", "dtmpc.h")

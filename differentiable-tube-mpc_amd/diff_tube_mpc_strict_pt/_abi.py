@@ -174,6 +174,7 @@ PROTOTYPES = {
     "dtmpc_dbas_init": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), I64, P, P, P]),
     "dtmpc_linearize": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), I64, P, P, P, P, P, P, P, P, P]),
     # include/dtmpc_control.h
+    "dtmpc_tape_cost": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), I64, P, P, P, P, P, P]),
     "dtmpc_tanh_cost_derivs": (
         C.c_int,
         [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), I64, P, P, P, P, P, P, P, P, P, P],

@@ -1,5 +1,6 @@
 /*
- * dtmpc_control.h — C ABI of libdtmpc.so, tanh-box control parameterisation (companion of dtmpc.h:
+ * dtmpc_control.h — C ABI of libdtmpc.so, tanh-box control parameterisation and the tape cost of
+ * core/ocp.py (companion of dtmpc.h:
  * same conventions -- caller-owned device buffers in SoA [rows][fields][B] layout, an explicit
  * hipStream_t, no allocation, DTMPC_ERR_BAD_ARG for invalid arguments before any device call).
  */
@@ -25,6 +26,13 @@ extern "C" {
 int dtmpc_tanh_cost_derivs(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, int64_t B,
                            const void* X, const void* Vdec, const void* Xref, const void* Uref,
                            void* U, void* dU, void* lx, void* lv, void* lvv, void* stream);
+
+/* Tape cost J = sum_{k<N} l(x_k, u_k) + phi(x_N) per trajectory:
+ *   replaces core/ocp.py:63-85 `total_cost` for the typed stage / terminal costs of dtmpc_cost (the
+ *   closures of core/tube_mpc.py:823-832 (TARGET), 875-885 (TRACK), run_nominal.py:297-324 (wrapped)).
+ *   X [N+1][4][B], U [N][2][B]; Xref [N+1][3][B] / Uref [N][2][B] read only for TRACK; J [B] out. */
+int dtmpc_tape_cost(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, int64_t B, const void* X,
+                    const void* U, const void* Xref, const void* Uref, void* J, void* stream);
 
 #ifdef __cplusplus
 }

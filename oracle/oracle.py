@@ -146,6 +146,17 @@ class Oracle:
                                            _p(U), _p(dU), _p(lx), _p(lv), _p(lvv))
         return {"u": aos(U), "dudv": aos(dU), "lx": aos(lx), "lv": aos(lv), "lvv": aos(lvv)}
 
+    def tape_cost(self, spec, cost, X, U, Xref=None, Uref=None):
+        """J = sum of stage costs + terminal cost per trajectory (core/ocp.py:63-85, typed costs)."""
+        X = self._a(X)
+        B = X.shape[0]
+        Xr = soa(self._a(Xref)[..., :3]) if Xref is not None else None
+        Ur = soa(self._a(Uref)) if Uref is not None else None
+        J = np.empty(B, self.dt)
+        self._f("oracle_tape_cost")(C.byref(spec), C.byref(cost), C.c_longlong(B), _p(soa(X)), _p(soa(self._a(U))),
+                                    _p(Xr), _p(Ur), _p(J))
+        return J
+
     def ilqr_solve(self, spec, cost, cfg, x0, V_init, Xref=None, Uref=None):
         x0 = self._a(x0)
         B, N = x0.shape[0], spec.horizon

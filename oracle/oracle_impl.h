@@ -1162,5 +1162,33 @@ void FN(oracle_tanh_cost_derivs)(const dtmpc_spec* sp, const dtmpc_cost* cp, lon
     }
 }
 
+/* total_cost core/ocp.py:63-85 with the typed stage / terminal costs (FN(traj_cost)): J = sum_k l_k + phi_N
+ * per trajectory, SoA tapes in (X [N+1][4][B], U [N][2][B], refs only for TRACK). */
+void FN(oracle_tape_cost)(const dtmpc_spec* sp, const dtmpc_cost* cp, long long B, const REAL* X, const REAL* U,
+                          const REAL* Xref, const REAL* Uref, REAL* J) {
+  SPEC_T s;
+  COST_T c;
+  FN(spec_from)(sp, &s);
+  FN(cost_from)(cp, &c);
+  const int N = s.N, trk = c.kind == DTMPC_COST_TRACK;
+  REAL* Xa = (REAL*)malloc(sizeof(REAL) * 4 * (N + 1));
+  REAL* Ua = (REAL*)malloc(sizeof(REAL) * 2 * N);
+  REAL* Xr = (REAL*)malloc(sizeof(REAL) * 3 * (N + 1));
+  REAL* Ur = (REAL*)malloc(sizeof(REAL) * 2 * N);
+  for (long long i = 0; i < B; ++i) {
+    FN(gather)(X, N + 1, 4, B, i, Xa);
+    FN(gather)(U, N, 2, B, i, Ua);
+    if (trk) {
+      FN(gather)(Xref, N + 1, 3, B, i, Xr);
+      FN(gather)(Uref, N, 2, B, i, Ur);
+    }
+    J[i] = FN(traj_cost)(&s, &c, Xa, Ua, trk ? Xr : NULL, trk ? Ur : NULL);
+  }
+  free(Xa);
+  free(Ua);
+  free(Xr);
+  free(Ur);
+}
+
 #undef SPEC_T
 #undef COST_T

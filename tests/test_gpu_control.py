@@ -103,3 +103,31 @@ def test_tanh_cost_derivs_tape_vs_oracle(dev, oracle_lib, tag, npdt, tdt, kind):
         got = np.transpose(o.cpu().numpy(), (2, 0, 1))
         assert np.isfinite(got).all(), k
         assert rel(got, want[k]) < tol, k
+
+
+@pytest.mark.parametrize("tag,npdt,tdt", DTYPES)
+def test_ocp_total_cost_and_rollout(dev, oracle_lib, tag, npdt, tdt):
+    """core.ocp.total_cost (dtmpc_tape_cost) vs the reference's total_cost with the paper closures
+    (golden ocp_*.npz) and vs the oracle; rollout_dynamics batched / unbatched vs core.ddp.rollout."""
+    from diff_tube_mpc_strict_pt.core import DubinsDBaSProblem
+    from diff_tube_mpc_strict_pt.core.ocp import rollout_dynamics, total_cost
+    from test_oracle_ocp import ocp_case
+
+    g, spec, nom, aux = ocp_case(tag)
+    tol = 1e-13 if tag == "f64" else 1e-6
+    t = lambda a: torch.as_tensor(np.asarray(a), dtype=tdt, device=dev)  # noqa: E731
+    X, U = t(g["X"]), t(g["U"])
+    J = total_cost(X=X, U=U, cost=nom).cpu().numpy()
+    np.testing.assert_allclose(J, g["J_nom"], rtol=tol)
+    o = oracle_lib.Oracle(npdt)
+    np.testing.assert_allclose(J, o.tape_cost(spec, nom.to_c(), g["X"], g["U"]), rtol=tol)
+    Ja = total_cost(X=X, U=U, cost=aux, X_ref=t(g["Xr"]), U_ref=t(g["Ur"])).cpu().numpy()
+    np.testing.assert_allclose(Ja, g["J_aux"], rtol=tol)
+    J1 = total_cost(X=X[2], U=U[2], cost=nom)
+    assert J1.dim() == 0 and abs(float(J1) - float(g["J_one"])) <= tol * abs(float(g["J_one"]))
+    prob = DubinsDBaSProblem(horizon=U.shape[1])
+    from diff_tube_mpc_strict_pt.core import rollout
+
+    Xr = rollout_dynamics(X[:, 0], U, f=prob)
+    assert torch.equal(Xr, rollout(prob, X[:, 0], U))
+    assert torch.equal(rollout_dynamics(X[3, 0], U[3], f=prob), Xr[3])
