@@ -456,9 +456,10 @@ __device__ __forceinline__ V kdot(const f4& K, V e0, V e1, V e2, V e3) {
 
 // ---------------------------------------------------------------------------------------------
 // the tapes one iLQR solve works on
-template <bool TRACK, bool G0 = false>
+template <bool TRACK, bool G0 = false, bool RG0 = G0>
 struct Solve {
-  static constexpr bool g0 = G0;  // gamma = 0: the compact gain records (Gains)
+  static constexpr bool g0 = G0;    // gamma = 0: the compact gain records (Gains)
+  static constexpr bool ric0 = RG0; // gamma = 0: the Riccati step without the barrier state's zero column
   Rsrc r;         // the workspace
   RA XA, UA;      // this solve's tape records (states + barrier state, controls)
   RA XRA, URA;    // TRACK: the nominal plan's records
@@ -639,45 +640,79 @@ struct RicP {
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc(float v) { return f2{v, v}; }
 
+// G0 (gamma = 0): A's column for the barrier state is exactly zero, so the recursion keeps V_xx's row /
+// column 3 at (0, 0, 0, 2 q_b) and V_x[3] at l_x[3] = 2 q_b b (the terms it would add are products with
+// exact zeros): row 3 of P, Q_xx and V_xx, the g * (.) products and B's zero entry b31 = dB(h') * 0 * dt
+// are dropped (-31 instructions per step).  The same sums, but with the zero terms gone the compiler
+// contracts two of them differently (l_u1 + b21 V_x2 and l_uu1 + s2 b21 become one fma each): an FMA
+// rounding of the same recursion, checked against the oracle builds like the rest of the kernel.
+template <bool G0>
 __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx, const float* lu, const float* lxx,
                                            const float* luu, float reg, RicP& R, float* K, float* kff) {
   const float a02 = J.a02, a12 = J.a12, a30 = J.a30, a31 = J.a31, a32 = J.a32, g = J.g;
   const float b00 = J.b00, b10 = J.b10, b21 = J.b21, b30 = J.b30, b31 = J.b31;
   const f2 A3 = f2{a30, a31};
   const float vx0 = R.Vx[0].x, vx1 = R.Vx[0].y, vx2 = R.Vx[1].x, vx3 = R.Vx[1].y;
+  // G0: V_xx row 3 = (0, 0 | 0, 2 q_b)
+  const f2 V30 = G0 ? f2{0.f, 0.f} : R.V[3][0];
+  const f2 V31 = G0 ? f2{0.f, lxx[3]} : R.V[3][1];
   // Q_x = l_x + A^T V_x ; Q_u = l_u + B^T V_x
   const f2 Qx01 = f2{lx[0], lx[1]} + fma2(A3, bc(vx3), R.Vx[0]);
   const float Qx2 = lx[2] + (a02 * vx0 + a12 * vx1 + vx2 + a32 * vx3);
-  const float Qx3 = lx[3] + g * vx3;
+  const float Qx3 = G0 ? lx[3] : lx[3] + g * vx3;
   const float Qu0 = lu[0] + (b00 * vx0 + b10 * vx1 + b30 * vx3);
-  const float Qu1 = lu[1] + (b21 * vx2 + b31 * vx3);
+  const float Qu1 = G0 ? lu[1] + b21 * vx2 : lu[1] + (b21 * vx2 + b31 * vx3);
   // P = A^T V_xx
   f2 P[4][2];
+  if (G0) {
+    P[0][0] = R.V[0][0];
+    P[1][0] = R.V[1][0];
+    P[2][0] = fma2(bc(a12), R.V[1][0], fma2(bc(a02), R.V[0][0], R.V[2][0]));
+    P[0][1] = fma2(bc(a30), V31, R.V[0][1]);
+    P[1][1] = fma2(bc(a31), V31, R.V[1][1]);
+    P[2][1] = fma2(bc(a32), V31, fma2(bc(a12), R.V[1][1], fma2(bc(a02), R.V[0][1], R.V[2][1])));
+  } else {
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    P[0][c] = fma2(bc(a30), R.V[3][c], R.V[0][c]);
-    P[1][c] = fma2(bc(a31), R.V[3][c], R.V[1][c]);
-    P[2][c] = fma2(bc(a32), R.V[3][c], fma2(bc(a12), R.V[1][c], fma2(bc(a02), R.V[0][c], R.V[2][c])));
-    P[3][c] = bc(g) * R.V[3][c];
+    for (int c = 0; c < 2; ++c) {
+      const f2 V3c = c ? V31 : V30;
+      P[0][c] = fma2(bc(a30), V3c, R.V[0][c]);
+      P[1][c] = fma2(bc(a31), V3c, R.V[1][c]);
+      P[2][c] = fma2(bc(a32), V3c, fma2(bc(a12), R.V[1][c], fma2(bc(a02), R.V[0][c], R.V[2][c])));
+      P[3][c] = bc(g) * V3c;
+    }
   }
   // Q_xx = P A + l_xx
+  constexpr int NR = G0 ? 3 : 4;  // G0: Q_xx row 3 = (0, 0, 0, 2 q_b)
   f2 Q[4][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const float p0 = P[i][0].x, p1 = P[i][0].y, p2 = P[i][1].x, p3 = P[i][1].y;
     Q[i][0] = fma2(A3, bc(p3), P[i][0]);
-    Q[i][1] = f2{a02 * p0 + a12 * p1 + p2 + a32 * p3, g * p3};
+    Q[i][1] = f2{a02 * p0 + a12 * p1 + p2 + a32 * p3, G0 ? 0.f : g * p3};
   }
   Q[0][0].x = lxx[0] + Q[0][0].x;
   Q[1][0].y = lxx[1] + Q[1][0].y;
   Q[2][1].x = lxx[2] + Q[2][1].x;
-  Q[3][1].y = lxx[3] + Q[3][1].y;
+  if (G0) {
+    Q[3][0] = f2{0.f, 0.f};
+    Q[3][1] = f2{0.f, lxx[3]};
+  } else {
+    Q[3][1].y = lxx[3] + Q[3][1].y;
+  }
   // S = B^T V_xx ; Q_ux = S A ; Q_uu = l_uu + S B
   f2 S[2][2];
+  if (G0) {
+    S[0][0] = fma2(bc(b10), R.V[1][0], bc(b00) * R.V[0][0]);
+    S[0][1] = fma2(bc(b30), V31, fma2(bc(b10), R.V[1][1], bc(b00) * R.V[0][1]));
+    S[1][0] = bc(b21) * R.V[2][0];
+    S[1][1] = bc(b21) * R.V[2][1];
+  } else {
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    S[0][c] = fma2(bc(b30), R.V[3][c], fma2(bc(b10), R.V[1][c], bc(b00) * R.V[0][c]));
-    S[1][c] = fma2(bc(b31), R.V[3][c], bc(b21) * R.V[2][c]);
+    for (int c = 0; c < 2; ++c) {
+      const f2 V3c = c ? V31 : V30;
+      S[0][c] = fma2(bc(b30), V3c, fma2(bc(b10), R.V[1][c], bc(b00) * R.V[0][c]));
+      S[1][c] = fma2(bc(b31), V3c, bc(b21) * R.V[2][c]);
+    }
   }
   f2 Qux[2][2];
   float Quu[2][2];
@@ -685,9 +720,9 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
   for (int a = 0; a < 2; ++a) {
     const float s0 = S[a][0].x, s1 = S[a][0].y, s2 = S[a][1].x, s3 = S[a][1].y;
     Qux[a][0] = fma2(A3, bc(s3), S[a][0]);
-    Qux[a][1] = f2{a02 * s0 + a12 * s1 + s2 + a32 * s3, g * s3};
+    Qux[a][1] = f2{a02 * s0 + a12 * s1 + s2 + a32 * s3, G0 ? 0.f : g * s3};
     Quu[a][0] = s0 * b00 + s1 * b10 + s3 * b30;
-    Quu[a][1] = s2 * b21 + s3 * b31;
+    Quu[a][1] = G0 ? s2 * b21 : s2 * b21 + s3 * b31;
   }
   Quu[0][0] = luu[0] + Quu[0][0];
   Quu[1][1] = luu[1] + Quu[1][1];
@@ -733,9 +768,10 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
     const f2 t3 = fma2(Qux[1][c], bc(kff[1]), Qux[0][c] * bc(kff[0]));
     R.Vx[c] = ((Qxp[c] + t1) + t2) + t3;
   }
+  if (G0) R.Vx[1].y = Qx3;  // V_x[3] = l_x[3]: its K-terms are products with K's zero column
   // V_xx = Q_xx + K^T Q_uu K + K^T Q_ux + Q_xu K: row i, column pair c, one fma chain
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const int ci = i >> 1;
     const float kq0 = (i & 1) ? KQ0[ci].y : KQ0[ci].x, kq1 = (i & 1) ? KQ1[ci].y : KQ1[ci].x;
     const float k0i = (i & 1) ? Kp[0][ci].y : Kp[0][ci].x, k1i = (i & 1) ? Kp[1][ci].y : Kp[1][ci].x;
@@ -835,7 +871,7 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     }
     float Kk[8], kk[2];
 #if DTMPC_FAST_RICPK
-    ok = riccati_pk(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
+    ok = riccati_pk<SV::ric0>(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
 #else
     ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
 #endif
@@ -1535,9 +1571,11 @@ __device__ __forceinline__ FP phase_p() {
   return p;
 }
 
-template <int M, int P, bool G0>
+// GM: 0 general, 1 gamma = 0 gain records, 2 gamma = 0 gain records + Riccati step (the default at gamma = 0)
+template <int M, int P, int GM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P, P)))
 tube_fast_kernel(FK kk) {
+  constexpr bool G0 = GM > 0, RG0 = GM > 1;
   (void)kk;  // read through kargs()
   __shared__ float red[kBlock / 64][DTMPC_TUBE_SUMS];
   const int B = kargs()->a.B, Bc = kargs()->a.Bc, i0 = kargs()->a.i0;
@@ -1576,7 +1614,7 @@ tube_fast_kernel(FK kk) {
     }
     {  // nominal MPC (fixed weights, :813-857)
       KArg* K = kargs();
-      Solve<false, G0> Sn;
+      Solve<false, G0, RG0> Sn;
       Sn.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
       Sn.XA = RA{K->a.oXn, cb * 16u, l16};
       Sn.UA = RA{K->a.oUn, cb * 8u, l8};
@@ -1603,7 +1641,7 @@ tube_fast_kernel(FK kk) {
       ca.qb = th[5];
       ca.t0 = ca.t1 = ca.t2 = 0.f;
     }
-    Solve<true, G0> Sa;
+    Solve<true, G0, RG0> Sa;
     {  // ancillary MPC tracking the nominal plan (:863-909)
       KArg* K = kargs();
       Sa.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
@@ -1825,10 +1863,13 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     a.whi[f] = float(cf->w_high[f]);
   }
   const int lanes = S->lanes;
-  // gamma = 0 (the paper's DBaS): the compact gain records (fk::Gains); DTMPC_FAST_G0=0 (environment,
-  // read at each call) keeps the general records, for the tests that compare both
-  bool g0 = p.gamma == 0.f;
-  if (const char* e = getenv("DTMPC_FAST_G0")) g0 = g0 && !(e[0] == '0' && e[1] == 0);
+  // gamma = 0 (the paper's DBaS): the compact gain records (fk::Gains) and the Riccati step without the
+  // barrier state's zero column (riccati_pk<true>).  DTMPC_FAST_G0 (environment, read at each call) = 0
+  // keeps the general records and recursion, = 1 the compact records with the general recursion: the
+  // tests compare 1 with 0 for exact equality (records) and the default with the oracle builds.
+  int g0 = p.gamma == 0.f ? 2 : 0;
+  if (const char* e = getenv("DTMPC_FAST_G0"))
+    if ((e[0] == '0' || e[0] == '1') && e[1] == 0) g0 = g0 < e[0] - '0' ? g0 : e[0] - '0';
   {
     const char* e = getenv("DTMPC_FAST_STAGGER");  // sleep rounds of ~8.1k cycles (A/B; default 0)
     a.stagger = e ? atoi(e) : 0;
@@ -1855,9 +1896,9 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
 #define FAST_CASE(m)                                                                                       \
   case m:                                                                                                  \
     if (lanes == 2) {                                                                                      \
-      if (g0) FAST_LAUNCH(m, 2, true); else FAST_LAUNCH(m, 2, false);                                      \
+      if (g0 == 2) FAST_LAUNCH(m, 2, 2); else if (g0) FAST_LAUNCH(m, 2, 1); else FAST_LAUNCH(m, 2, 0);     \
     } else {                                                                                               \
-      if (g0) FAST_LAUNCH(m, 1, true); else FAST_LAUNCH(m, 1, false);                                      \
+      if (g0 == 2) FAST_LAUNCH(m, 1, 2); else if (g0) FAST_LAUNCH(m, 1, 1); else FAST_LAUNCH(m, 1, 0);     \
     }                                                                                                      \
     break;
     switch (sp->n_obstacles) {

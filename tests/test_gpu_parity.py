@@ -627,7 +627,10 @@ def test_tube_step_fast_gamma0_records(dev, lanes, monkeypatch):
     fast kernel then keeps K and k in one 32-byte record per step (dtmpc_fast.hip fk::Gains).  The
     general 40-byte records (DTMPC_FAST_G0=0) must give the same values -- an exact zero term dropped
     from the feedback sum changes nothing but, at most, the sign of a zero -- over two closed-loop
-    steps: states, tapes, log rows, partial sums and the shared theta."""
+    steps: states, tapes, log rows, partial sums and the shared theta.  DTMPC_FAST_G0=1 is the compact
+    records with the general Riccati step; the default at gamma = 0 also drops the barrier state's zero
+    column from the recursion (riccati_pk<true>, an FMA rounding of it), which test_tube_step_vs_oracle
+    checks against the oracle builds."""
     import dataclasses
 
     from diff_tube_mpc_strict_pt.core import TubeMPC
