@@ -35,3 +35,37 @@ def test_oracle_tape_cost_vs_reference(oracle_lib, tag, dt):
     J = o.tape_cost(spec, aux.to_c(), g["X"], g["U"], Xref=g["Xr"], Uref=g["Ur"])
     np.testing.assert_allclose(J, g["J_aux"], rtol=tol)
     assert abs(float(g["J_one"]) - float(g["J_nom"][2])) <= tol * abs(float(g["J_one"]))
+
+
+def test_tape_cost_abi_arguments_validated():
+    """dtmpc_tape_cost rejects bad arguments with DTMPC_ERR_BAD_ARG before any HIP call."""
+    import ctypes as C
+
+    from diff_tube_mpc_strict_pt import _abi, _lib
+
+    lib = _lib.load()
+    g, spec, nom, aux = ocp_case("f64")
+    sp, cn, ca = spec, nom.to_c(), aux.to_c()
+    rc = lib.dtmpc_tape_cost(_abi.F64, C.byref(sp), C.byref(ca), 4, 1, 1, None, None, 1, None)
+    assert rc == _abi.ERR_BAD_ARG and b"Xref" in lib.dtmpc_last_error()
+    rc = lib.dtmpc_tape_cost(_abi.F64, C.byref(sp), C.byref(cn), 4, 1, 1, None, None, None, None)
+    assert rc == _abi.ERR_BAD_ARG and b"NULL" in lib.dtmpc_last_error()
+    rc = lib.dtmpc_tape_cost(_abi.F64, C.byref(sp), C.byref(cn), 0, 1, 1, None, None, 1, None)
+    assert rc == _abi.ERR_BAD_ARG and b"batch" in lib.dtmpc_last_error()
+    rc = lib.dtmpc_tape_cost(9, C.byref(sp), C.byref(cn), 4, 1, 1, None, None, 1, None)
+    assert rc == _abi.ERR_BAD_ARG and b"dtype" in lib.dtmpc_last_error()
+
+
+def test_ocp_host_side_checks():
+    """core.ocp refuses host tensors (no CPU fallback) and mismatched horizons before any launch."""
+    import torch
+
+    from diff_tube_mpc_strict_pt.core import DubinsDBaSProblem, QuadraticCost
+    from diff_tube_mpc_strict_pt.core.ocp import rollout_dynamics, total_cost
+
+    X = torch.zeros(2, 6, 4)
+    U = torch.zeros(2, 5, 2)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        total_cost(X=X, U=U, cost=QuadraticCost())
+    with pytest.raises(ValueError, match="horizon"):
+        rollout_dynamics(X[:, 0], U, f=DubinsDBaSProblem(horizon=7))
