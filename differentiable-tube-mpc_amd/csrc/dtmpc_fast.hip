@@ -380,7 +380,9 @@ __device__ __forceinline__ float h_grad(const FP& p, float px, float py, float& 
 
 // DBaS-augmented Dubins step (fhat_vec): x' = dubins_step(x, u) (core/systems/dubins.py:26-45),
 // b' = B(h(x')) - gamma (B(h(x)) - b) (core/barrier.py:75-108); Bc carries B(h(x))
-template <int M, class V>
+// G0 (gamma = 0): b' = B(h(x')) -- the general form adds (-0) * (B(h(x)) - b), which changes nothing
+// for finite values
+template <int M, bool G0 = false, class V>
 __device__ __forceinline__ void fhat(const FP& p, V& x0, V& x1, V& x2, V& b, V u0, V u1, V& Bc) {
   DTMPC_NOCONTRACT
   V sn, cs;
@@ -390,7 +392,7 @@ __device__ __forceinline__ void fhat(const FP& p, V& x0, V& x1, V& x2, V& b, V u
   x1 = ffma(dv, sn, x1);
   x2 = ffma(V(p.dt), u1, x2);
   const V Bn = vbarrier(p, h_sm<M>(p, x0, x1));
-  b = ffma(V(-p.gamma), Bc - b, Bn);
+  b = G0 ? Bn : ffma(V(-p.gamma), Bc - b, Bn);
   Bc = Bn;
 }
 
@@ -593,7 +595,7 @@ __device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const fl
     const float u0 = vclamp(v0, p.umin0, p.umax0), u1 = vclamp(v1, p.umin1, p.umax1);
     S.stu(k, f2{u0, u1});
     if (want_cost) J = J + stage<TRACK>(c, s0, s1, s2, sb, u0, u1, R.x, R.y, R.z, Q.x, Q.y);
-    fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
+    fhat<M, SV::g0>(p, s0, s1, s2, sb, u0, u1, Bc);
     S.stx(k + 1, f4{s0, s1, s2, sb});
   }
   if (!want_cost) return 0.f;
@@ -1059,8 +1061,12 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
   }
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
-    C.ab[q] = ffma(f2(-p.gamma), C.Bp[q] - C.ab[q], Bn[q]);
-    C.Bp[q] = Bn[q];
+    if (G0) {  // b' = B(h(x')) (fhat<M, true>)
+      C.ab[q] = Bn[q];
+    } else {
+      C.ab[q] = ffma(f2(-p.gamma), C.Bp[q] - C.ab[q], Bn[q]);
+      C.Bp[q] = Bn[q];
+    }
   }
 }
 
@@ -1252,7 +1258,7 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
     if (__builtin_isnan(s0 + u0 + u1)) S.stx(k + 1, f4{s0, s1, s2, sb});
 #else
     S.stu(k, f2{u0, u1});
-    fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
+    fhat<M, SV::g0>(p, s0, s1, s2, sb, u0, u1, Bc);
     S.stx(k + 1, f4{s0, s1, s2, sb});
 #endif
   };
