@@ -77,3 +77,18 @@ def test_box_controls_host_side():
     assert p.u_max == (10.0, np.pi) and p.active_tol == 1e-8
     with pytest.raises(ValueError):
         BoxTanhControl(u_min=(1.0, 0.0), u_max=(1.0, 1.0))
+
+
+def test_tanh_mirror_refuses_host_tensors():
+    """core.control / core.cost_derivs have no CPU fallback: host tensors raise before any launch."""
+    import torch
+
+    from diff_tube_mpc_strict_pt.core import BoxTanhControl, nominal_cost_derivs
+
+    ctrl = BoxTanhControl(u_min=(-10.0, -np.pi), u_max=(10.0, np.pi))
+    v = torch.zeros(3, 2, dtype=torch.float64)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        ctrl.u(v)
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        nominal_cost_derivs(x_hat=torch.zeros(3, 4, dtype=torch.float64), v=v, target=(1.0, 1.0, 0.0),
+                            Q=(1.0, 1.0, 0.0), R=(1.0, 1.0), qb=1.0, ctrl=ctrl)
