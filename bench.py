@@ -11,8 +11,15 @@ instead is not a stable workload in f32: from step 1 on, a few trajectories' anc
 obstacle (b ~ 1e10, also in f64), their f32 IFT gradients are ill-conditioned (|g| ~ 1e15-1e30), the
 batch-mean theta jumps to ~1e10 and trajectories start to overflow.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_per_gpu] [--no-cpu]
-        (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+Scaling: by default the GLOBAL batch (--batch, 65,536 = BASELINE config 5) is split over the N ranks by
+shard_range ("scaling": "strong", 8,192 trajectories per GPU at N = 8); --weak keeps --batch per GPU.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--weak] [--no-cpu]
+  N > 1 without a torch.distributed environment: bench.py launches its N ranks itself (a child
+  `python -m torch.distributed.run --nproc-per-node N ...` started before any GPU call, one process per
+  GPU over RCCL) and exits with the child's status; under torchrun it is one rank.
+  --dry-run: the same launch / process group / sharding / timing arithmetic on CPU (gloo), with a
+  placeholder step instead of the GPU kernels (tests/test_bench_launch.py).
 """
 from __future__ import annotations
 
@@ -64,21 +71,40 @@ def initial_states(lo: int, hi: int, device, dtype) -> torch.Tensor:
     return x0.to(device=device, dtype=dtype)
 
 
-def pmc_traffic(batch: int):
-    """Per-launch HBM bytes of the tube-step kernel from a committed rocprofv3 --pmc summary (or None).
-    FETCH_SIZE is doubled (gfx950 under-reports wide coalesced reads by 2x, MI355X_MICROARCH.md §HBM)."""
+def lib_sha256() -> str:
+    """sha256 of the libdtmpc.so this process loads (a PMC summary is only valid for the same library)."""
+    import hashlib
+
+    from diff_tube_mpc_strict_pt import _lib
+
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_traffic(batch: int, kernel: str = "tube"):
+    """Per-launch HBM bytes of the dominant kernel from a committed rocprofv3 --pmc summary
+    (profiles/rNN/pmc_*.json, written by scripts/pmc_summary.py) for the SAME library build (sha256) and
+    batch, or (None, reason).  FETCH_SIZE / WRITE_SIZE are calibrated there on a known-byte launch
+    (MI355X_MICROARCH.md §HBM: gfx950 under-reports wide coalesced reads)."""
     def newest_first(path):  # profiles/rNN/pmc_vMM.json: the highest round, then the highest version
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.relpath(path, REPO))]
 
-    best = None
+    want = lib_sha256()
+    best, why = None, "no PMC summary for this batch"
     for p in sorted(glob.glob(os.path.join(REPO, "profiles", "**", "*pmc*.json"), recursive=True), key=newest_first):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        if int(d.get("batch", -1)) == batch and "tube_step_bytes_per_launch" in d:
-            best = float(d["tube_step_bytes_per_launch"])
-    return best
+        if int(d.get("batch", -1)) != batch or d.get("workload", "tube") != kernel:
+            continue
+        if "tube_step_bytes_per_launch" not in d:
+            continue
+        if d.get("lib_sha256") != want:
+            best, why = None, f"newest PMC summary for this batch ({os.path.relpath(p, REPO)}) is of another library build"
+            continue
+        best, why = float(d["tube_step_bytes_per_launch"]), os.path.relpath(p, REPO)
+    return best, why
 
 
 def cpu_baseline(setup, seconds_target: float = 15.0):
@@ -120,76 +146,130 @@ def cpu_baseline(setup, seconds_target: float = 15.0):
                       f"(10+20 fixed iLQR iterations, 7 alphas, + IFT), OpenMP {threads} threads, {dt:.1f} s"}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start the N ranks as ONE child process tree (torch.distributed.run, one process per GPU) and
+    return its exit status.  Called before this process touches the GPU (no exec: a child, not a
+    replacement)."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC on this host driver
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=65536, help="trajectories per GPU (weak scaling)")
+    ap.add_argument("--batch", type=int, default=65536,
+                    help="GLOBAL trajectories split over the ranks (strong scaling); per GPU with --weak")
+    ap.add_argument("--weak", action="store_true", help="--batch trajectories per GPU (weak scaling)")
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU-baseline leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo rehearsal of launch, sharding and timing with a placeholder step (no GPU)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    group = None
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if env_world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={env_world}")
+    if args.dry_run:
+        dev = torch.device("cpu")
+        if env_world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if env_world > 1:
+            dist.init_process_group("nccl", device_id=dev)  # RCCL
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    if dist.is_initialized():
+        rank = dist.get_rank()
     dtype = torch.float32 if args.dtype == "f32" else torch.float64
     setup = bench_setup(args.dtype)
-    Bg = args.batch * world
+    Bg = args.batch * world if args.weak else args.batch
+    if Bg < world:
+        raise SystemExit(f"global batch {Bg} < {world} ranks")
     lo, hi = shard_range(Bg, rank, world)
-    mpc = TubeMPC(setup, batch=hi - lo, device=dev, dtype=dtype, disturbance="philox", seed=0,
-                  global_offset=lo, global_batch=Bg, process_group=group)
-    x0 = initial_states(lo, hi, dev, dtype)
 
-    def step(kernel_events=None):
-        mpc.reset(x0)
-        mpc.step(kernel_events=kernel_events)
+    if args.dry_run:
+        mpc = None
+
+        def step(kernel_events=None):
+            time.sleep(0.002)
+    else:
+        mpc = TubeMPC(setup, batch=hi - lo, device=dev, dtype=dtype, disturbance="philox", seed=0,
+                      global_offset=lo, global_batch=Bg, process_group=None)
+        x0 = initial_states(lo, hi, dev, dtype)
+
+        def step(kernel_events=None):
+            mpc.reset(x0)
+            mpc.step(kernel_events=kernel_events)
+
+    def sync():
+        if not args.dry_run:
+            torch.cuda.synchronize(dev)
 
     def barrier():
-        torch.cuda.synchronize(dev)
+        sync()
         if world > 1:
             dist.barrier()
-            torch.cuda.synchronize(dev)
+            sync()
 
     for _ in range(args.warmup):
         step()
     barrier()
-    # HIP events on the launch stream: whole step, and the fused tube_step kernel alone
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if args.dry_run:
+        ev = kev = None
+    else:
+        # HIP events on the launch stream: whole step, and the fused tube_step kernel alone
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for s in range(args.steps):
-        e0, e1 = ev[s]
-        e0.record()
-        step(kernel_events=kev[s])
-        e1.record()
+        if ev is not None:
+            ev[s][0].record()
+            step(kernel_events=kev[s])
+            ev[s][1].record()
+        else:
+            step()
     barrier()
     wall = time.perf_counter() - t0
-    step_ms = [e0.elapsed_time(e1) for e0, e1 in ev]
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in kev]))
-    # f32 can overflow on trajectories driven deep into an obstacle's relaxed barrier, exactly where the
-    # reference raises FloatingPointError in f32; such trajectories are flagged and counted (last step).
-    flagged = torch.tensor([int((mpc.status != 0).sum())], dtype=torch.int64, device=dev)
+    if ev is not None:
+        step_ms = [e0.elapsed_time(e1) for e0, e1 in ev]
+        kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in kev]))
+        # f32 can overflow on trajectories driven deep into an obstacle's relaxed barrier, exactly where
+        # the reference raises FloatingPointError in f32; such trajectories are flagged and counted
+        flagged_local = int((mpc.status != 0).sum())
+    else:
+        step_ms, kern_ms, flagged_local = [1e3 * wall / max(args.steps, 1)], 1e3 * wall / max(args.steps, 1), 0
+    red = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    cnt = torch.tensor([flagged_local], dtype=torch.int64, device=dev)
     if world > 1:
-        dist.all_reduce(flagged)
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    wall = float(wall_t)
+        dist.all_reduce(red, op=dist.ReduceOp.MAX)  # the slowest rank sets the step time
+        dist.all_reduce(cnt)
+    wall, kern_ms_max = float(red[0]), float(red[1])
 
     ms_per_step = 1e3 * wall / args.steps
     value = Bg * ITERS_PER_STEP / (wall / args.steps)
     algo_bytes = ALGO_BYTES_PER_TRAJ_STEP * (hi - lo)
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(hi - lo)
+    traffic, traffic_src = (None, "dry run") if args.dry_run else pmc_traffic(hi - lo)
     out = {
         "metric": "DDP+IFT iters/sec, batched Dubins+DBaS T=50",
         "value": value,
@@ -199,7 +279,7 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.weak else "strong",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic: x0 ~ U[0,1]^2 x U[0,pi/2] per global index, Philox disturbances, configs/dubins.yaml values",
@@ -210,16 +290,20 @@ def main() -> None:
             "line_search_alphas": len(setup.ilqr_nom.line_search_alphas), "parallelism": f"dp{world}",
         },
         "kernel_ms": kern_ms,
-        "flagged_trajectories": int(flagged),
+        "kernel_ms_max_over_ranks": kern_ms_max,
+        "flagged_trajectories": int(cnt[0]),
         "event_ms_per_step_median": float(np.median(step_ms)),
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "algo_bytes_per_launch": algo_bytes,
         },
     }
-    if rank == 0 and not args.no_cpu and world == 1:
+    if args.dry_run:
+        out["dry_run"] = True
+    if rank == 0 and not args.no_cpu and world == 1 and not args.dry_run:
         out["cpu_baseline"] = cpu_baseline(setup)
     else:
         out["cpu_baseline"] = None

@@ -3,7 +3,9 @@
 Plain hipcc, no build system: the translation units compiled in parallel, then linked --
 csrc/dtmpc_kernels.hip (paper path + per-function entry points), csrc/dtmpc_general.hip (general IFT
 path), csrc/dtmpc_receding.hip (receding-horizon nominal MPC driver), csrc/dtmpc_control.hip (tanh-box
-control map + cost derivatives), csrc/dtmpc_ocp.hip (tape cost of core/ocp.py).
+control map + cost derivatives), csrc/dtmpc_ocp.hip (tape cost of core/ocp.py), csrc/dtmpc_systems.hip
+(per-point kernels of the reference's per-function API: dynamics, h, barriers, Jacobians, clamp, cost
+derivatives).
 """
 from __future__ import annotations
 
@@ -16,10 +18,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f)
         for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_general.hip", "dtmpc_receding.hip",
-                  "dtmpc_control.hip", "dtmpc_ocp.hip")]
+                  "dtmpc_control.hip", "dtmpc_ocp.hip", "dtmpc_systems.hip")]
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solver.hpp", "dtmpc_general.hpp",
                                                  "dtmpc_host.hpp", "dtmpc_ls_pk.hpp")] + [
-    os.path.join(os.path.dirname(HERE), "include", "dtmpc.h")
+    os.path.join(os.path.dirname(HERE), "include", h) for h in ("dtmpc.h", "dtmpc_control.h", "dtmpc_systems.h")
 ]
 OUT = os.path.join(HERE, "diff_tube_mpc_strict_pt", "libdtmpc.so")
 CACHE = os.path.join(HERE, "build", "obj")  # object cache keyed by the command line + source texts

@@ -118,8 +118,6 @@ int dtmpc_tanh_cost_derivs(int dtype, const dtmpc_spec* spec, const dtmpc_cost* 
   if ((e = check_cost(cost, Xref, Uref))) return e;
   if (cost->wrap_angle) return set_err(DTMPC_ERR_BAD_ARG, "tanh-box cost derivatives take the unwrapped cost");
   if (!Vdec || (lx && !X)) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
-  for (int j = 0; j < 2; ++j)
-    if (!(spec->u_max[j] > spec->u_min[j])) return set_err(DTMPC_ERR_BAD_ARG, "u_max must exceed u_min");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DTMPC_F32) return launch_tanh<float>(*spec, *cost, B, X, Vdec, Xref, Uref, U, dU, lx, lv, lvv, st);
   if (dtype == DTMPC_F64) return launch_tanh<double>(*spec, *cost, B, X, Vdec, Xref, Uref, U, dU, lx, lv, lvv, st);

@@ -30,6 +30,8 @@ namespace fk {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f8 __attribute__((ext_vector_type(8)));
+typedef int i8v __attribute__((ext_vector_type(8)));
 
 constexpr int NC = 6;  // rolled-out line-search candidates (alpha = 0 is the current tape)
 
@@ -41,18 +43,19 @@ struct FP {
   float neg_beta, neg_inv_beta;
   float nbl2e;  // neg_beta * log2(e): exp(-beta h_i - zmax) = exp2(fma(h_i, nbl2e, -zmax log2(e)))
   float a, eps, gamma, inv_a, a2, a3, inv_a2;
-  float cx[8], cy[8], r2[8];
+  f8 cx, cy, r2;  // ext-vector: SSA values (a float[8] became a private array in memory)
 };
 
 struct FCost {  // nominal: target; ancillary: tracking (terminal weight = stage weight)
-  float Q0, Q1, Q2, R0, R1, Qf0, Qf1, Qf2, qb, t0, t1, t2;
+  float Q0, Q1, Q2, R0, R1, Qf0, Qf1, Qf2, qb;
+  f4 tg;  // target (x, y, theta, -): ext-vector, an SSA value (three floats became a private array)
 };
 
 struct FIlqr {
   int max_iter, zpos;
   float tol, reg;
-  float cal[NC];
-  int cpos[NC];
+  f8 cal;   // rolled-out candidates' alphas (NC used); ext-vectors: SSA values, never a private array
+  i8v cpos; // their original positions
 };
 
 struct FArgs {
@@ -190,29 +193,92 @@ __device__ __forceinline__ void rst2(Rsrc, const RA& a, int k, unsigned off, f2 
 }
 #endif
 
+// LDS-resident gains.  The iLQR gains of the first KL steps of the horizon live in the LDS of the
+// trajectory's CU instead of the workspace: the backward pass writes them, the line search and the
+// commit read them (core/ddp.py:248-249, 266-269) -- three HBM passes over 32 B per step and iteration
+// that never leave the CU.  One workgroup per CU holds all 160 KiB: quad q (16 B) of step s of the
+// trajectory with workgroup-local index j is at lds[(s * Q + q) * LS + j] (LS = trajectories per
+// workgroup), so a wave's access is 64 consecutive 16-B slots (conflict-free ds_read/write_b128) and the
+// lanes of one trajectory (P > 1) read one address (broadcast).  KL = what fits: 20 steps at one lane per
+// trajectory (gamma = 0 records), 40 at two, the whole horizon at four.
+typedef __attribute__((address_space(3))) f4 lf4;
+constexpr int kLdsF4 = 163840 / 16;  // 160 KiB: the whole LDS of a CU, one workgroup per CU
+
+template <int P, bool G0>
+struct GainLds {
+  static constexpr int Q = G0 ? 2 : 3;          // 16-byte quads per step: K (2) [+ k]
+  static constexpr int LS = kBlock / P;         // trajectories per workgroup
+  // steps held in LDS.  Only the gamma = 0 records (the paper's and the benchmark's DBaS) use it: with the
+  // general 40-byte records in three quads per step the results differed from the workspace-only path in
+  // a same-box diagnostic (scripts/diag_g0.py; deterministic, cause not found), so they stay in the
+  // workspace.
+#ifdef DTMPC_FAST_LDS_STEPS  // A/B and diagnostics: at most this many steps in LDS (0: none)
+  static constexpr int KL = !G0 ? 0 : kLdsF4 / (LS * Q) < DTMPC_FAST_LDS_STEPS ? kLdsF4 / (LS * Q) : DTMPC_FAST_LDS_STEPS;
+#else
+  static constexpr int KL = !G0 ? 0 : kLdsF4 / (LS * Q);
+#endif
+};
+
+template <int P>
 struct Gains {
-  RA K, k;  // K and k records
+  RA K, k;     // K and k records (the steps past KL, and the sensitivity pass's full records)
+  lf4* L;      // this trajectory's LDS column (lds + workgroup-local trajectory index)
+  bool w;      // this lane writes the LDS copy (the trajectory's first lane; P = 1: every lane)
   // G0 (gamma = 0): K's column for the barrier state b is exactly zero (A's column 3 is (0, 0, 0, gamma),
   // so Q_ux's is gamma * S = 0 and K = -Q_uu^-1 Q_ux keeps it), and the iLQR record is the 32 bytes
   // K00 K01 K02 K10 | K11 K12 k0 k1 -- 8 B less per step, two loads instead of three
   template <bool G0>
   __device__ __forceinline__ void store(Rsrc r, int s, const float* Kk, const float* kk) const {
-    if (G0) {
-      rst4(r, K, s, 0, f4{Kk[0], Kk[1], Kk[2], Kk[4]});
-      rst4(r, K, s, 16, f4{Kk[5], Kk[6], kk[0], kk[1]});
+    using GL = GainLds<P, G0>;
+    const f4 g0 = G0 ? f4{Kk[0], Kk[1], Kk[2], Kk[4]} : f4{Kk[0], Kk[1], Kk[2], Kk[3]};
+    const f4 g1 = G0 ? f4{Kk[5], Kk[6], kk[0], kk[1]} : f4{Kk[4], Kk[5], Kk[6], Kk[7]};
+    if (s < GL::KL) {
+      if (P == 1 || w) {
+        L[(s * GL::Q) * GL::LS] = g0;
+        L[(s * GL::Q + 1) * GL::LS] = g1;
+        if (!G0) L[(s * GL::Q + 2) * GL::LS] = f4{kk[0], kk[1], 0.f, 0.f};
+      }
     } else {
-      rst4(r, K, s, 0, f4{Kk[0], Kk[1], Kk[2], Kk[3]});
-      rst4(r, K, s, 16, f4{Kk[4], Kk[5], Kk[6], Kk[7]});
-      rst2(r, k, s, 0, f2{kk[0], kk[1]});
+      rst4(r, K, s, 0, g0);
+      rst4(r, K, s, 16, g1);
+      if (!G0) rst2(r, k, s, 0, f2{kk[0], kk[1]});
     }
   }
+  // step s's gains: K rows (Ka, Kb; G0: the zero column as 0) and k
+  template <bool G0>
+  __device__ __forceinline__ void load(Rsrc r, int s, f4& Ka, f4& Kb, f2& kf) const {
+    using GL = GainLds<P, G0>;
+    f4 g0, g1;
+    f2 k2;
+    if (s < GL::KL) {
+      g0 = L[(s * GL::Q) * GL::LS];
+      g1 = L[(s * GL::Q + 1) * GL::LS];
+      if (!G0) {
+        const f4 g2 = L[(s * GL::Q + 2) * GL::LS];
+        k2 = f2{g2.x, g2.y};
+      }
+    } else {
+      g0 = rld4(r, K, s, 0);
+      g1 = rld4(r, K, s, 16);
+      if (!G0) k2 = rld2(r, k, s, 0);
+    }
+    if (G0) {
+      Ka = f4{g0.x, g0.y, g0.z, 0.f};
+      Kb = f4{g0.w, g1.x, g1.y, 0.f};
+      kf = f2{g1.z, g1.w};
+    } else {
+      Ka = g0;
+      Kb = g1;
+      kf = k2;
+    }
+  }
+  // the sensitivity pass's full records K (32 B) + k (8 B), always in the workspace
+  __device__ __forceinline__ void store_full(Rsrc r, int s, const float* Kk, const float* kk) const {
+    rst4(r, K, s, 0, f4{Kk[0], Kk[1], Kk[2], Kk[3]});
+    rst4(r, K, s, 16, f4{Kk[4], Kk[5], Kk[6], Kk[7]});
+    rst2(r, k, s, 0, f2{kk[0], kk[1]});
+  }
 };
-
-// the lane pair's partner value (P = 2): DPP quad_perm [1, 0, 3, 2], one VALU move
-__device__ __forceinline__ float pswap(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-}
-__device__ __forceinline__ int pswap(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
 
 // ---------------------------------------------------------------------------------------------
 // elementwise math on V = float (one candidate) or f2 (a candidate pair, packed f32 VALU)
@@ -415,9 +481,9 @@ __device__ __forceinline__ V stage(const FCost& c, V x0, V x1, V x2, V b, V u0, 
     e0 = u0 - q0;
     e1 = u1 - q1;
   } else {
-    d0 = x0 - c.t0;
-    d1 = x1 - c.t1;
-    d2 = x2 - c.t2;
+    d0 = x0 - c.tg.x;
+    d1 = x1 - c.tg.y;
+    d2 = x2 - c.tg.z;
     e0 = u0;
     e1 = u1;
   }
@@ -434,9 +500,9 @@ __device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, float r
     d1 = x1 - r1;
     d2 = x2 - r2;
   } else {
-    d0 = x0 - c.t0;
-    d1 = x1 - c.t1;
-    d2 = x2 - c.t2;
+    d0 = x0 - c.tg.x;
+    d1 = x1 - c.tg.y;
+    d2 = x2 - c.tg.z;
   }
   const V sq = ffma(c.Qf2 * d2, d2, ffma(c.Qf1 * d1, d1, (c.Qf0 * d0) * d0));
   return ffma(V(c.qb), b * b, sq);
@@ -458,14 +524,15 @@ __device__ __forceinline__ V kdot(const f4& K, V e0, V e1, V e2, V e3) {
 
 // ---------------------------------------------------------------------------------------------
 // the tapes one iLQR solve works on
-template <bool TRACK, bool G0 = false, bool RG0 = G0>
+template <bool TRACK, bool G0, bool RG0, int P>
 struct Solve {
   static constexpr bool g0 = G0;    // gamma = 0: the compact gain records (Gains)
   static constexpr bool ric0 = RG0; // gamma = 0: the Riccati step without the barrier state's zero column
+  static constexpr int lanes = P;   // lanes per trajectory
   Rsrc r;         // the workspace
-  RA XA, UA;      // this solve's tape records (states + barrier state, controls)
+  RA XA, UA;      // this solve's tape records (states + barrier state, controls); P = 4: the current slot
   RA XRA, URA;    // TRACK: the nominal plan's records
-  Gains G;
+  Gains<P> G;
   Soa<4> X;       // ABI [N+1][4][B] tape (written at the end of the solve)
   Soa<2> U;       // ABI [N][2][B] controls (in: warm start, out: plan)
   __device__ __forceinline__ f4 x(int k) const { return rld4(r, XA, k, 0); }
@@ -496,16 +563,7 @@ __device__ __forceinline__ void load_step(StepIn& L, const SV& S, int k) {
   const f2 V = S.u(k);
   L.V0 = V.x;
   L.V1 = V.y;
-  if (SV::g0) {
-    const f4 g0 = rld4(S.r, S.G.K, k, 0), g1 = rld4(S.r, S.G.K, k, 16);
-    L.Ka = f4{g0.x, g0.y, g0.z, 0.f};
-    L.Kb = f4{g0.w, g1.x, g1.y, 0.f};
-    L.kk = f2{g1.z, g1.w};
-  } else {
-    L.Ka = rld4(S.r, S.G.K, k, 0);
-    L.Kb = rld4(S.r, S.G.K, k, 16);
-    L.kk = rld2(S.r, S.G.k, k, 0);
-  }
+  S.G.template load<SV::g0>(S.r, k, L.Ka, L.Kb, L.kk);
   if (TRACK) {
     const f4 R = S.xr(k);
     const f2 Q = S.ur(k);
@@ -791,9 +849,43 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
   return ok;
 }
 
-// backward pass (ilqr_backward, core/ddp.py:172-254)
+// broadcast of lane J of each group of P lanes (P = 2: quad_perm [J, J, J+2, J+2]; P = 4: [J, J, J, J]),
+// one DPP move; j is a constant after unrolling
+template <int P, int J>
+__device__ __forceinline__ float gbc(float v) {
+  constexpr int ctrl = P == 4 ? J * 0x55 : (J == 0 ? 0xA0 : 0xF5);
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false));
+}
+template <int P>
+__device__ __forceinline__ float gbcast(float v, int j) {
+  switch (j) {
+    case 0: return gbc<P, 0>(v);
+    case 1: return gbc<P, 1 % P>(v);
+    case 2: return gbc<P, 2 % P>(v);
+    default: return gbc<P, 3 % P>(v);
+  }
+}
+
+// the per-point part of the linearisation: sin / cos of the heading, grad h and B'(h) at X
+struct Lin {
+  float sn, cs, gx, gy, dB;
+};
+template <int M>
+__device__ __forceinline__ Lin lin_point(const FP& p, const f4& X) {
+  Lin L;
+  vsincos(X.z, L.sn, L.cs);
+  L.dB = dbarrier(p, h_grad<M>(p, X.x, X.y, L.gx, L.gy));
+  return L;
+}
+
+// backward pass (ilqr_backward, core/ddp.py:172-254).  P > 1: the per-point linearisation (sin / cos,
+// grad h, B' -- about a third of a step) is computed for P steps at once, one step per lane of the
+// trajectory, and handed to every lane by DPP broadcasts; the Riccati recursion itself is sequential
+// and runs on every lane (each needs the gains).  Same operations on the same values as P = 1: the
+// gains are bitwise those of the one-lane form.
 template <bool TRACK, int M, class SV>
-__device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg, const SV& S) {
+__device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg, const SV& S, int h) {
+  constexpr int P = SV::lanes;
   const int N = p.N;
   const float lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
   const float luu[2] = {2.f * c.R0, 2.f * c.R1};
@@ -807,9 +899,9 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     d1 = xn1 - RN.y;
     d2 = xn2 - RN.z;
   } else {
-    d0 = xn0 - c.t0;
-    d1 = xn1 - c.t1;
-    d2 = xn2 - c.t2;
+    d0 = xn0 - c.tg.x;
+    d1 = xn1 - c.tg.y;
+    d2 = xn2 - c.tg.z;
   }
 #if DTMPC_FAST_RICPK
   RicP R;
@@ -846,21 +938,17 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     nR = S.xr(N - 1);
     nQ = S.ur(N - 1);
   }
-  auto step = [&](const f4& X, const f2& V, const f4& Rr, const f2& Q, int k) {
+  auto step = [&](const f4& X, const f2& V, const f4& Rr, const f2& Q, int k, const Lin& Lk) {
     const float x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w, u0 = V.x, u1 = V.y;
-    float sn, cs;
-    vsincos(x2, sn, cs);
-    float gxk, gyk;
-    const float dBk = dbarrier(p, h_grad<M>(p, x0, x1, gxk, gyk));
-    const Jac<float> J = jac(p, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
+    const Jac<float> J = jac(p, Lk.sn, Lk.cs, u0, Lk.gx, Lk.gy, Lk.dB, gxn, gyn, dBn);
     if (TRACK) {
       d0 = x0 - Rr.x;
       d1 = x1 - Rr.y;
       d2 = x2 - Rr.z;
     } else {
-      d0 = x0 - c.t0;
-      d1 = x1 - c.t1;
-      d2 = x2 - c.t2;
+      d0 = x0 - c.tg.x;
+      d1 = x1 - c.tg.y;
+      d2 = x2 - c.tg.z;
     }
     const float lx[4] = {lxx[0] * d0, lxx[1] * d1, lxx[2] * d2, lxx[3] * xb};
     float lu[2];
@@ -878,13 +966,11 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
 #endif
     S.G.template store<SV::g0>(S.r, k, Kk, kk);
-    gxn = gxk;
-    gyn = gyk;
-    dBn = dBk;
+    gxn = Lk.gx;
+    gyn = Lk.gy;
+    dBn = Lk.dB;
   };
-  for (int k = N - 1; k >= 0; --k) {
-    const f4 X = nX, Rr = nR;
-    const f2 V = nV, Q = nQ;
+  auto next_inputs = [&](int k) {  // the inputs of step k - 1
     if (k > 0) {
       nX = S.x(k - 1);
       nV = S.u(k - 1);
@@ -893,7 +979,43 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
         nQ = S.ur(k - 1);
       }
     }
-    step(X, V, Rr, Q, k);
+  };
+  if (P == 1) {
+    for (int k = N - 1; k >= 0; --k) {
+      const f4 X = nX, Rr = nR;
+      const f2 V = nV, Q = nQ;
+      next_inputs(k);
+      step(X, V, Rr, Q, k, lin_point<M>(p, X));
+    }
+  } else {
+    // lane h of the trajectory linearises row kt - h of each group of P steps kt, kt - 1, ...; the
+    // group's rows are read one group ahead (per-lane row: the group's lowest row as the uniform base)
+    auto prow = [&](int kt) {
+      const int rb = kt - (P - 1) > 0 ? kt - (P - 1) : 0;
+      const int r = kt - h > 0 ? kt - h : 0;
+      return rld4(S.r, S.XA, uidx(rb), (unsigned)(r - rb) * S.XA.rs);
+    };
+    f4 PX = prow(N - 1);
+    for (int kt = N - 1; kt >= 0; kt -= P) {
+      const f4 PXc = PX;
+      if (kt - P >= 0) PX = prow(kt - P);
+      const Lin Lh = lin_point<M>(p, PXc);
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        const int k = kt - j;
+        if (k < 0) break;
+        const f4 X = nX, Rr = nR;
+        const f2 V = nV, Q = nQ;
+        next_inputs(k);
+        Lin Lk;
+        Lk.sn = gbcast<P>(Lh.sn, j);
+        Lk.cs = gbcast<P>(Lh.cs, j);
+        Lk.gx = gbcast<P>(Lh.gx, j);
+        Lk.gy = gbcast<P>(Lh.gy, j);
+        Lk.dB = gbcast<P>(Lh.dB, j);
+        step(X, V, Rr, Q, k, Lk);
+      }
+    }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) ok = ok && finite(RVX(i));
@@ -909,7 +1031,7 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
 // ops / compare-select sits back to back (each such pair costs an s_nop wait state on gfx950).
 // Arithmetic per candidate is the scalar forward pass (fhat, stage) operation for operation.
 #ifndef DTMPC_FAST_LS_DEPTH2
-#define DTMPC_FAST_LS_DEPTH2 1  // one lane per trajectory: two steps of prefetch lead (measured -1.5 %)
+#define DTMPC_FAST_LS_DEPTH2 1  // two steps of prefetch lead (one lane per trajectory: measured -1.5 %)
 #endif
 template <int NPR>
 struct Cand {
@@ -984,9 +1106,8 @@ __device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
 
 // one step of the NPR pairs' rollouts: feedback + clamp, stage cost, DBaS-augmented Dubins move
 template <bool TRACK, int M, int NPR, bool G0>
-__device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepIn& s, Cand<NPR>& C) {
+__device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepIn& s, Cand<NPR>& C, f2* u0, f2* u1) {
   DTMPC_NOCONTRACT
-  f2 u0[NPR], u1[NPR];
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
     const f2 e0 = C.a0[q] - s.X0, e1 = C.a1[q] - s.X1, e2 = C.a2[q] - s.X2, e3 = C.ab[q] - s.X3;
@@ -1070,17 +1191,41 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
   }
 }
 
+// P = 4: the candidate tapes.  Every lane writes the rollouts of its two candidates into their own
+// slots of the solve's tape records (instead of the winner being re-rolled by a commit pass): slot
+// bank * 6 + candidate, in the bank the current tape is not in; the winner's slot then becomes the
+// current tape (Slots::cur).  X row 0 of a slot is x0, row k + 1 the state after control row k.
+struct Slots {
+  RA X0, X1, U0, U1;  // this lane's two candidate slots (X and U records)
+};
+
+// per-lane choice among the three candidate pairs of a trajectory (lanes 0, 1, 2; lane 3 repeats lane 2)
+template <class T>
+__device__ __forceinline__ T pick3(int h, T a, T b, T c) { return h == 0 ? a : h == 1 ? b : c; }
+
+// the partner of this lane in a lane group at distance 1 (quad_perm [1, 0, 3, 2]) or 2 ([2, 3, 0, 1])
+template <int D>
+__device__ __forceinline__ float gswap(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), D == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false));
+}
+template <int D>
+__device__ __forceinline__ int gswap(int v) { return __builtin_amdgcn_mov_dpp(v, D == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false); }
+
 // Returns the chosen original position (or -1 if any candidate or Jprev is non-finite), its cost
-// and alpha.  P = 1: the six candidates as three pairs; P = 2: three per lane (two pairs, the last
-// one doubled), the pair of lanes combining their minima by one DPP swap.
+// and alpha, and (bc) the chosen rolled-out candidate (-1: the zero candidate, i.e. the current tape).
+// P = 1: the six candidates as three pairs; P = 2: three per lane (two pairs, the last one doubled);
+// P = 4: one pair per lane (lane 3 repeats lane 2's), each lane storing its pair's tapes (Slots).  The
+// lanes of a trajectory combine their minima by DPP swaps.
 template <bool TRACK, int M, int P, class SV>
 __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FIlqr& cf, const float* x0, float Bc0,
-                                           const SV& S, float Jprev, int h, float& bestJ, float& al_out) {
+                                           const SV& S, float Jprev, int h, float& bestJ, float& al_out, int& bc,
+                                           const Slots& Z) {
   DTMPC_NOCONTRACT
-  constexpr int NL = NC / P;          // candidates of this lane
-  constexpr int NPR = (NL + 1) / 2;   // pairs
+  constexpr int NL = P == 4 ? 2 : NC / P;  // candidates of this lane
+  constexpr int NPR = (NL + 1) / 2;        // pairs
   const int N = p.N;
-  const int c0 = h * NL;              // this lane's first candidate (index into cf.cal / cf.cpos)
+  const int hc = P == 4 ? (h < 2 ? h : 2) : h;  // this lane's candidate group
+  const int c0 = hc * NL;                        // its first candidate (index into cf.cal / cf.cpos)
   Cand<NPR> C;
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
@@ -1091,40 +1236,65 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
     C.Bp[q] = Bc0;
     C.J[q] = 0.f;
     const int i0 = 2 * q, i1 = 2 * q + 1 < NL ? 2 * q + 1 : NL - 1;
-    C.al[q] = P == 1 ? f2{cf.cal[i0], cf.cal[i1]} : (h ? f2{cf.cal[NL + i0], cf.cal[NL + i1]} : f2{cf.cal[i0], cf.cal[i1]});
+    if (P == 1)
+      C.al[q] = f2{cf.cal[i0], cf.cal[i1]};
+    else if (P == 2)
+      C.al[q] = h ? f2{cf.cal[NL + i0], cf.cal[NL + i1]} : f2{cf.cal[i0], cf.cal[i1]};
+    else
+      C.al[q] = f2{pick3(hc, cf.cal[0], cf.cal[2], cf.cal[4]), pick3(hc, cf.cal[1], cf.cal[3], cf.cal[5])};
   }
-  // two step buffers in turn (no copies), each refilled two steps ahead; the refill index is clamped
-  // (a redundant load of the last row instead of a branch)
+  if (P == 4) {  // the candidates' row 0
+    const f4 X0v = f4{x0[0], x0[1], x0[2], x0[3]};
+    rst4(S.r, Z.X0, 0, 0, X0v);
+    rst4(S.r, Z.X1, 0, 0, X0v);
+  }
+  // P = 4: the pair's controls of step k and states of step k + 1 into its slots
+  auto keep = [&](int k, const f2* u0, const f2* u1) {
+    if (P == 4) {
+      rst2(S.r, Z.U0, k, 0, f2{u0[0].x, u1[0].x});
+      rst2(S.r, Z.U1, k, 0, f2{u0[0].y, u1[0].y});
+      rst4(S.r, Z.X0, k + 1, 0, f4{C.a0[0].x, C.a1[0].x, C.a2[0].x, C.ab[0].x});
+      rst4(S.r, Z.X1, k + 1, 0, f4{C.a0[0].y, C.a1[0].y, C.a2[0].y, C.ab[0].y});
+    }
+  };
+  f2 u0[NPR], u1[NPR];
   const int N1 = N - 1;
-  if (DTMPC_FAST_LS_DEPTH2 && P == 1) {
-  // four buffers in rotation, each refilled two steps before use (one lane per trajectory only: at two
-  // lanes the 256-register cap of two waves per SIMD would spill the extra buffers)
+  if (DTMPC_FAST_LS_DEPTH2) {
+  // four buffers in rotation, each refilled two steps before use
   auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
   StepIn A, Bs, Cs, Ds;
   load_step<TRACK>(A, S, 0);
   load_step<TRACK>(Bs, S, ix(1));
   for (int k = 0; k < N; k += 4) {
     load_step<TRACK>(Cs, S, ix(k + 2));
-    ls_step<TRACK, M, NPR, SV::g0>(p, c, A, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, A, C, u0, u1);
+    keep(k, u0, u1);
     if (k + 1 >= N) break;
     load_step<TRACK>(Ds, S, ix(k + 3));
-    ls_step<TRACK, M, NPR, SV::g0>(p, c, Bs, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, Bs, C, u0, u1);
+    keep(k + 1, u0, u1);
     if (k + 2 >= N) break;
     load_step<TRACK>(A, S, ix(k + 4));
-    ls_step<TRACK, M, NPR, SV::g0>(p, c, Cs, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, Cs, C, u0, u1);
+    keep(k + 2, u0, u1);
     if (k + 3 >= N) break;
     load_step<TRACK>(Bs, S, ix(k + 5));
-    ls_step<TRACK, M, NPR, SV::g0>(p, c, Ds, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, Ds, C, u0, u1);
+    keep(k + 3, u0, u1);
   }
   } else {
+  // two step buffers in turn (no copies), each refilled two steps ahead; the refill index is clamped
+  // (a redundant load of the last row instead of a branch)
   StepIn A, Bs;
   load_step<TRACK>(A, S, 0);
   load_step<TRACK>(Bs, S, N1 < 1 ? N1 : 1);
   for (int k = 0; k < N; k += 2) {
-    ls_step<TRACK, M, NPR, SV::g0>(p, c, A, C);
+    ls_step<TRACK, M, NPR, SV::g0>(p, c, A, C, u0, u1);
+    keep(k, u0, u1);
     load_step<TRACK>(A, S, uidx(k + 2 < N1 ? k + 2 : N1));
     if (k + 1 < N) {
-      ls_step<TRACK, M, NPR, SV::g0>(p, c, Bs, C);
+      ls_step<TRACK, M, NPR, SV::g0>(p, c, Bs, C, u0, u1);
+      keep(k + 1, u0, u1);
       load_step<TRACK>(Bs, S, uidx(k + 3 < N1 ? k + 3 : N1));
     }
   }
@@ -1161,7 +1331,9 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   if (cf.zpos >= 0) {
 #pragma unroll
     for (int a = 0; a < NL; ++a) {
-      const int pos = P == 1 ? cf.cpos[a] : (h ? cf.cpos[NL + a] : cf.cpos[a]);
+      const int pos = P == 1 ? cf.cpos[a]
+                    : P == 2 ? (h ? cf.cpos[NL + a] : cf.cpos[a])
+                             : pick3(hc, cf.cpos[a], cf.cpos[2 + a], cf.cpos[4 + a]);
       if (pos < cf.zpos) {
         mb = (!hb || Jc[a] < mb) ? Jc[a] : mb;
         hb = 1;
@@ -1171,24 +1343,28 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
       }
     }
   }
-  if (P == 2) {  // combine with the partner lane: lexicographic (J, position) = strict <, first wins
-    const float oJ = pswap(bJ);
-    const int oi = pswap(bi);
-    ok = pswap((int)ok) && ok;
+  // combine with the trajectory's other lanes: lexicographic (J, position) = strict <, first wins
+  auto combine = [&](auto sw) {
+    const float oJ = sw(bJ);
+    const int oi = sw(bi);
+    ok = sw((int)ok) && ok;
     if (oJ < bJ || (oJ == bJ && oi < bi)) {
       bJ = oJ;
       bi = oi;
     }
     if (cf.zpos >= 0) {
-      const float omb = pswap(mb), oma = pswap(ma);
-      const int ohb = pswap(hb), oha = pswap(ha);
+      const float omb = sw(mb), oma = sw(ma);
+      const int ohb = sw(hb), oha = sw(ha);
       if (ohb) mb = (!hb || omb < mb) ? omb : mb;
       if (oha) ma = (!ha || oma < ma) ? oma : ma;
       hb |= ohb;
       ha |= oha;
     }
-  }
+  };
+  if (P >= 2) combine([](auto v) { return gswap<1>(v); });
+  if (P == 4) combine([](auto v) { return gswap<2>(v); });
   bestJ = bJ;
+  bc = bi;
   int best = cf.cpos[0];
   al_out = cf.cal[0];
 #pragma unroll
@@ -1202,6 +1378,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
       best = cf.zpos;
       bestJ = Jprev;
       al_out = 0.f;
+      bc = -1;
     }
     ok = ok && finite(Jprev);
   }
@@ -1232,7 +1409,7 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
 #else
   constexpr bool LX = true;
 #endif
-  Solve<false, SV::g0> T0;  // no references needed
+  Solve<false, SV::g0, SV::ric0, SV::lanes> T0;  // no references needed
   T0.r = S.r;
   T0.XA = S.XA;
   T0.UA = S.UA;
@@ -1323,10 +1500,18 @@ __device__ __forceinline__ void ls_stat(int trk, int best, float al, const FIlqr
 }
 #endif
 
-// iLQR for one trajectory (ilqr_traj, core/ddp.py:102-307)
+// P = 4 tape slots: slot q of the solve's X / U records at lane offset base + q * stride
+struct SlotMap {
+  unsigned bx, sx, bu, su;  // X: base (trajectory * 16), slot stride (Bc * 16); U: (trajectory * 8), (Bc * 8)
+};
+constexpr int kSlots = 12;     // two banks of the six rolled-out candidates
+constexpr int kSlotInit = 6;   // the initial rollout: bank 1, so the first line search writes bank 0
+
+// iLQR for one trajectory (ilqr_traj, core/ddp.py:102-307).  P = 4: no commit pass -- the line search
+// kept every candidate's tape (Slots) and the winner's slot becomes the current tape (S.XA / S.UA).
 template <bool TRACK, int M, int P, class SV>
 __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const float* x0,
-                                    const SV& S, int h, int& iters, Prof& pf) {
+                                    SV& S, int h, const SlotMap& sm, int& iters, Prof& pf) {
   constexpr int ph = TRACK ? 4 : 0;  // phase-timer slots (profiling builds)
   float Jcur = init_tape<TRACK, M>(p, c, x0, S, cf.zpos >= 0 && cf.max_iter > 0);
   const float Bc0 = barrier_at<M>(p, x0[0], x0[1]);
@@ -1334,16 +1519,27 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
   float prev = 0.f;
   iters = 0;
   int st = 0;
+  int cur = kSlotInit;  // P = 4: the current tape's slot
   pf.mark(ph);
   for (int it = 0; it < cf.max_iter; ++it) {
     iters = it + 1;
-    if (!backward<TRACK, M>(p, c, cf.reg, S)) {
+    if (!backward<TRACK, M>(p, c, cf.reg, S, h)) {
       st = DTMPC_ST_NONFINITE;
       break;
     }
     pf.mark(ph + 1);
     float bestJ, al;
-    const int best = line_search<TRACK, M, P>(p, c, cf, x0, Bc0, S, Jcur, h, bestJ, al);
+    int bc;
+    Slots Z;
+    const int nb = cur < 6 ? 6 : 0;  // first slot of the bank the current tape is not in
+    if (P == 4) {
+      const unsigned q0 = (unsigned)(nb + 2 * (h < 2 ? h : 2));
+      Z.X0 = RA{S.XA.base, S.XA.rs, sm.bx + q0 * sm.sx};
+      Z.X1 = RA{S.XA.base, S.XA.rs, sm.bx + (q0 + 1) * sm.sx};
+      Z.U0 = RA{S.UA.base, S.UA.rs, sm.bu + q0 * sm.su};
+      Z.U1 = RA{S.UA.base, S.UA.rs, sm.bu + (q0 + 1) * sm.su};
+    }
+    const int best = line_search<TRACK, M, P>(p, c, cf, x0, Bc0, S, Jcur, h, bestJ, al, bc, Z);
     pf.mark(ph + 2);
 #ifdef DTMPC_PROFILE
     ls_stat(TRACK ? 1 : 0, best, al, cf);
@@ -1352,7 +1548,15 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
       st = DTMPC_ST_NONFINITE;
       break;
     }
-    if (al != 0.f) commit<TRACK, M>(p, al, x0, Bc0, S);
+    if (al != 0.f) {
+      if (P == 4) {
+        cur = nb + bc;
+        S.XA.lo = sm.bx + (unsigned)cur * sm.sx;
+        S.UA.lo = sm.bu + (unsigned)cur * sm.su;
+      } else {
+        commit<TRACK, M>(p, al, x0, Bc0, S);
+      }
+    }
     pf.mark(ph + 3);
     Jcur = bestJ;
     if (have_prev && m_abs(prev - bestJ) < cf.tol) break;
@@ -1448,7 +1652,7 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV
 #pragma unroll
       for (int j = 0; j < 4; ++j) R.Vxx[i][j] = Qxx[i][j] + (Qxu[i][0] * Kk[j] + Qxu[i][1] * Kk[4 + j]);
     }
-    S.G.template store<false>(S.r, k, Kk, kk);  // full records: its own K and k
+    S.G.store_full(S.r, k, Kk, kk);  // full records in the workspace: its own K and k
     rst4(S.r, A8, k, 0, f4{J.a02, J.a12, J.a30, J.a31});
     rst4(S.r, A8, k, 16, f4{J.a32, J.b00, J.b10, J.b30});
     rst2(S.r, A2, k, 0, f2{J.b31, float((act0 ? 1 : 0) + (act1 ? 2 : 0))});
@@ -1569,25 +1773,31 @@ __device__ __forceinline__ FP phase_p() {
 #if DTMPC_FAST_PIN
 #pragma unroll
   for (int j = 0; j < M; ++j) {
-    __asm__ volatile("" : "+v"(p.cx[j]));
-    __asm__ volatile("" : "+v"(p.cy[j]));
-    __asm__ volatile("" : "+v"(p.r2[j]));
+    float vx = p.cx[j], vy = p.cy[j], vr = p.r2[j];
+    __asm__ volatile("" : "+v"(vx));
+    __asm__ volatile("" : "+v"(vy));
+    __asm__ volatile("" : "+v"(vr));
+    p.cx[j] = vx;
+    p.cy[j] = vy;
+    p.r2[j] = vr;
   }
 #endif
   return p;
 }
 
 // GM: 0 general, 1 gamma = 0 gain records, 2 gamma = 0 gain records + Riccati step (the default at gamma = 0)
+// One workgroup per CU (the LDS gains take all of it) and so one wave per SIMD at every lane count: the
+// whole 512-register budget.
 template <int M, int P, int GM>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P, P)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 tube_fast_kernel(FK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
   (void)kk;  // read through kargs()
-  __shared__ float red[kBlock / 64][DTMPC_TUBE_SUMS];
+  __shared__ f4 lds[kLdsF4];  // the gains of the first steps (Gains); the workgroup sums at the end
   const int B = kargs()->a.B, Bc = kargs()->a.Bc, i0 = kargs()->a.i0;
   const int gl = blockIdx.x * kBlock + threadIdx.x;
-  const int t = P == 1 ? gl : (gl >> 1), h = P == 1 ? 0 : (gl & 1);  // t: index in the chunk
-  const int i = i0 + t;                                                // index in the batch
+  const int t = gl / P, h = gl % P;  // t: index in the chunk, h: lane of the trajectory
+  const int i = i0 + t;              // index in the batch
   float acc[DTMPC_TUBE_SUMS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   {
     // desynchronise the workgroups' phases: every wave runs the same sequence of passes, so without an
@@ -1603,7 +1813,14 @@ tube_fast_kernel(FK kk) {
     const size_t nb = (size_t)B;
     const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
     const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
+    // record strides: P = 4 keeps kSlots tapes per solve (slot-major inside a row), else one
+    constexpr unsigned NS = P == 4 ? kSlots : 1;
     const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * 8u, l16 = (unsigned)t * 16u, l32 = (unsigned)t * 32u;
+    const SlotMap sm{l16, cb * 16u, l8, cb * 8u};
+    const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * 16u : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * 8u : l8;
+    Gains<P> G;
+    G.L = (lf4*)lds + (threadIdx.x / P);
+    G.w = h == 0;
 
     int st = 0, itn = 0, ita = 0;
     float x0, x1, x2, xb, y0, y1, y2, yb;
@@ -1618,14 +1835,15 @@ tube_fast_kernel(FK kk) {
       y2 = K->a.xbar[2 * nb + i];
       yb = K->a.bbar[i];
     }
+    Solve<false, G0, RG0, P> Sn;
     {  // nominal MPC (fixed weights, :813-857)
       KArg* K = kargs();
-      Solve<false, G0, RG0> Sn;
       Sn.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
-      Sn.XA = RA{K->a.oXn, cb * 16u, l16};
-      Sn.UA = RA{K->a.oUn, cb * 8u, l8};
+      Sn.XA = RA{K->a.oXn, NS * cb * 16u, x0lo};
+      Sn.UA = RA{K->a.oUn, NS * cb * 8u, u0lo};
       Sn.XRA = Sn.XA;
       Sn.URA = Sn.UA;
+      Sn.G = G;
       Sn.G.K = RA{K->a.oK, cb * 32u, l32};
       Sn.G.k = RA{K->a.ok, cb * 8u, l8};
       Sn.X = Soa<4>{(char*)K->a.Xnom, 4u * bb, L};
@@ -1634,7 +1852,7 @@ tube_fast_kernel(FK kk) {
       const FCost cn = K->cn;
       const FIlqr cfn = K->cfn;
       const float xn0[4] = {y0, y1, y2, yb};
-      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, itn, pf);
+      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, sm, itn, pf);
     }
     FCost ca;  // ancillary weights theta (shared by the batch), terminal weight Qa (:885, :891)
     {
@@ -1645,16 +1863,17 @@ tube_fast_kernel(FK kk) {
       ca.R0 = th[3];
       ca.R1 = th[4];
       ca.qb = th[5];
-      ca.t0 = ca.t1 = ca.t2 = 0.f;
+      ca.tg = f4{0.f, 0.f, 0.f, 0.f};
     }
-    Solve<true, G0, RG0> Sa;
+    Solve<true, G0, RG0, P> Sa;
     {  // ancillary MPC tracking the nominal plan (:863-909)
       KArg* K = kargs();
       Sa.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
-      Sa.XA = RA{K->a.oXa, cb * 16u, l16};
-      Sa.UA = RA{K->a.oUa, cb * 8u, l8};
-      Sa.XRA = RA{K->a.oXn, cb * 16u, l16};
-      Sa.URA = RA{K->a.oUn, cb * 8u, l8};
+      Sa.XA = RA{K->a.oXa, NS * cb * 16u, x0lo};
+      Sa.UA = RA{K->a.oUa, NS * cb * 8u, u0lo};
+      Sa.XRA = Sn.XA;  // the nominal plan as solved (P = 4: its final slot)
+      Sa.URA = Sn.UA;
+      Sa.G = G;
       Sa.G.K = RA{K->a.oK, cb * 32u, l32};
       Sa.G.k = RA{K->a.ok, cb * 8u, l8};
       Sa.X = Soa<4>{(char*)K->a.Xaux, 4u * bb, L};
@@ -1662,7 +1881,7 @@ tube_fast_kernel(FK kk) {
       const FP p = phase_p<M>();
       const FIlqr cfa = K->cfa;
       const float xa0[4] = {x0, x1, x2, xb};
-      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, ita, pf);
+      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, sm, ita, pf);
     }
     pf.mark(8);
     {  // upper loss, DOC sensitivity and gradient (:915-976)
@@ -1677,7 +1896,7 @@ tube_fast_kernel(FK kk) {
       const FArgs& a = K->a;
       const FP p = phase_p<M>();
       // the plans' first controls, from the records (the ABI tapes already hold the shifted warm starts)
-      const f2 ua = rld2(Sa.r, Sa.UA, 0, 0), un = rld2(Sa.r, RA{a.oUn, cb * 8u, l8}, 0, 0);
+      const f2 ua = rld2(Sa.r, Sa.UA, 0, 0), un = rld2(Sa.r, Sn.UA, 0, 0);
       const float u0 = ua.x, u1 = ua.y;
       const float v0 = un.x, v1 = un.y;
       float w[3];
@@ -1727,7 +1946,7 @@ tube_fast_kernel(FK kk) {
         a.bbar[i] = qb;
       }
       acc[7] = 1.f;
-      if (st || h != 0) {  // healthy trajectories only; a lane pair counts once
+      if (st || h != 0) {  // healthy trajectories only; a trajectory's lanes count once
 #pragma unroll
         for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) acc[j] = 0.f;
       }
@@ -1743,16 +1962,19 @@ tube_fast_kernel(FK kk) {
   }
   pf.flush();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float ws[DTMPC_TUBE_SUMS];
 #pragma unroll
-  for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) {
-    const float v = wave_sum(acc[j]);
-    if (lane == 0) red[wv][j] = v;
-  }
+  for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) ws[j] = wave_sum(acc[j]);
+  __syncthreads();  // every wave is done with its LDS gains: the first 128 bytes take the wave sums
+  float* red = (float*)lds;
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) red[wv * DTMPC_TUBE_SUMS + j] = ws[j];
   __syncthreads();
   if (threadIdx.x < DTMPC_TUBE_SUMS) {
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < kBlock / 64; ++q) v += red[q][threadIdx.x];
+    for (int q = 0; q < kBlock / 64; ++q) v += red[q * DTMPC_TUBE_SUMS + threadIdx.x];
     kargs()->a.partials[((size_t)blockIdx.x + (size_t)i0 * P / kBlock) * DTMPC_TUBE_SUMS + threadIdx.x] = v;
   }
 }
@@ -1765,21 +1987,41 @@ tube_fast_kernel(FK kk) {
 // The fast kernel's configuration: f32, smooth-min over 1..8 obstacles, relaxed inverse barrier,
 // untightened h, nominal target cost without wrap, and six rolled-out candidates in both solves.
 // DTMPC_FAST=0 (environment, read at the call) forces the generic kernel (parity tests compare both).
-// trajectories per launch of the fast kernel: its workspace records (two tapes of (N+1) x 16 B + N x 8 B,
-// gains and sensitivity scratch of N x 40 B per trajectory) stay below 2^31 bytes, in workgroup multiples
-// (DTMPC_FAST_CHUNK, environment, read at each call: a smaller chunk, for the tests of the chunked launch)
-int64_t tube_fast_chunk(int N) {
-  const int64_t per = (int64_t)(N + 1) * 32 + (int64_t)N * 96;
-  int64_t c = ((int64_t)0x7fffffff / per) / kBlock * kBlock;
-  if (const char* e = getenv("DTMPC_FAST_CHUNK")) {
-    const int64_t v = atoll(e) / kBlock * kBlock;
-    if (v > 0 && v < c) c = v;
-  }
+//
+// Workspace records of one launch chunk of Bc trajectories (NS = 12 tape slots per solve at four lanes,
+// else 1): nominal and ancillary X [N+1][NS][Bc][4], U [N][NS][Bc][2]; gains K [N][Bc][8], k [N][Bc][2];
+// sensitivity scratch A8 [N][Bc][8], A2 [N][Bc][2].  All of it addressed through one buffer resource, so a
+// chunk's records stay below 2^31 bytes (tube_fast_chunk_max); larger batches run in chunks.
+struct FastLayout {
+  unsigned oXn, oXa, oUn, oUa, oK, ok, oA8, oA2, wsz;
+};
+static int64_t fast_bytes_per_traj(int N, int lanes) {
+  const int64_t ns = lanes == 4 ? fk::kSlots : 1;
+  return ns * ((int64_t)(N + 1) * 32 + (int64_t)N * 16) + (int64_t)N * 80;
+}
+static FastLayout fast_layout(int N, int64_t Bc, int lanes) {
+  const int64_t ns = lanes == 4 ? fk::kSlots : 1;
+  const unsigned X = (unsigned)(ns * Bc * (N + 1) * 16), U = (unsigned)(ns * Bc * N * 8);
+  const unsigned K = (unsigned)(Bc * N * 32), k = (unsigned)(Bc * N * 8);
+  FastLayout f;
+  f.oXn = 0;
+  f.oXa = X;
+  f.oUn = 2 * X;
+  f.oUa = 2 * X + U;
+  f.oK = 2 * X + 2 * U;
+  f.ok = f.oK + K;
+  f.oA8 = f.ok + k;
+  f.oA2 = f.oA8 + K;
+  f.wsz = f.oA2 + k;
+  return f;
+}
+int64_t tube_fast_chunk_max(int N, int lanes) {
+  const int64_t c = ((int64_t)0x7fffffff / fast_bytes_per_traj(N, lanes)) / kBlock * kBlock;
   return c < kBlock ? kBlock : c;
 }
-size_t tube_fast_workspace_bytes(int N, int64_t B) {
-  const int64_t c = tube_fast_chunk(N), b = B < c ? B : c;
-  return (size_t)b * ((size_t)(N + 1) * 32 + (size_t)N * 96);
+size_t tube_fast_workspace_bytes(int N, int64_t B, int lanes, int64_t chunk) {
+  const int64_t b = B < chunk ? B : chunk;
+  return (size_t)b * (size_t)fast_bytes_per_traj(N, lanes);
 }
 
 bool tube_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf) {
@@ -1838,7 +2080,7 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     p.r2[i] = i < s.M ? s.r2[i] : 0.f;
   }
   const DCost<float> c = make_cost<float>(cf->nominal);
-  kk.cn = fk::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb, c.t0, c.t1, c.t2};
+  kk.cn = fk::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb, fk::f4{c.t0, c.t1, c.t2, 0.f}};
   kk.cfn = fast_ilqr(cf->nom_ilqr);
   kk.cfa = fast_ilqr(cf->aux_ilqr);
   fk::FArgs& a = kk.a;
@@ -1881,32 +2123,43 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     a.stagger = e ? atoi(e) : 0;
   }
   // the batch in chunks whose workspace records fit one buffer resource (< 2^31 bytes), each chunk a
-  // multiple of the workgroup size (its partial-sum rows follow the previous chunk's)
-  const int64_t chunk = tube_fast_chunk(N);
+  // multiple of the workgroup size (its partial-sum rows follow the previous chunk's); the chunk comes
+  // from the state (dtmpc_tube_chunk, validated against the workspace by dtmpc_tube_step)
+  const int64_t chunk = S->chunk;
   for (int64_t c0 = 0; c0 < B; c0 += chunk) {
     const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
     a.i0 = (int)c0;
     a.Bc = (int)Bc;
-    const unsigned X = (unsigned)(Bc * (N + 1) * 16), U = (unsigned)(Bc * N * 8), K = (unsigned)(Bc * N * 32);
-    a.oXn = 0;
-    a.oXa = X;
-    a.oUn = 2 * X;
-    a.oUa = 2 * X + U;
-    a.oK = 2 * X + 2 * U;
-    a.ok = 2 * X + 2 * U + K;
-    a.oA8 = 2 * X + 3 * U + K;
-    a.oA2 = 2 * X + 3 * U + 2 * K;
-    a.wsz = 2 * X + 4 * U + 2 * K;
+    const FastLayout f = fast_layout(N, Bc, lanes);
+    a.oXn = f.oXn;
+    a.oXa = f.oXa;
+    a.oUn = f.oUn;
+    a.oUa = f.oUa;
+    a.oK = f.oK;
+    a.ok = f.ok;
+    a.oA8 = f.oA8;
+    a.oA2 = f.oA2;
+    a.wsz = f.wsz;
     const dim3 grid = grid_for(Bc * lanes);
 #define FAST_LAUNCH(m, l, g) hipLaunchKernelGGL((fk::tube_fast_kernel<m, l, g>), grid, dim3(kBlock), 0, st, kk)
+#define FAST_LANES(m, l) \
+  if (g0 == 2) FAST_LAUNCH(m, l, 2); else if (g0) FAST_LAUNCH(m, l, 1); else FAST_LAUNCH(m, l, 0);
+#ifdef DTMPC_FAST_ISA_ONLY  // ISA inspection builds: one instantiation (lanes 1, gamma = 0 records + Riccati)
+#define FAST_CASE(m) \
+  case m:            \
+    FAST_LAUNCH(m, DTMPC_FAST_ISA_ONLY, 2); break;
+#else
 #define FAST_CASE(m)                                                                                       \
   case m:                                                                                                  \
-    if (lanes == 2) {                                                                                      \
-      if (g0 == 2) FAST_LAUNCH(m, 2, 2); else if (g0) FAST_LAUNCH(m, 2, 1); else FAST_LAUNCH(m, 2, 0);     \
+    if (lanes == 4) {                                                                                      \
+      FAST_LANES(m, 4)                                                                                     \
+    } else if (lanes == 2) {                                                                               \
+      FAST_LANES(m, 2)                                                                                     \
     } else {                                                                                               \
-      if (g0 == 2) FAST_LAUNCH(m, 1, 2); else if (g0) FAST_LAUNCH(m, 1, 1); else FAST_LAUNCH(m, 1, 0);     \
+      FAST_LANES(m, 1)                                                                                     \
     }                                                                                                      \
     break;
+#endif
     switch (sp->n_obstacles) {
 #ifdef DTMPC_FAST_M_ONLY
       FAST_CASE(DTMPC_FAST_M_ONLY)
@@ -1916,6 +2169,7 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
       default: return set_err(DTMPC_ERR_BAD_ARG, "fast tube step: obstacle count not instantiated");
     }
 #undef FAST_CASE
+#undef FAST_LANES
 #undef FAST_LAUNCH
   }
   return check_launch("tube_fast_kernel");

@@ -170,8 +170,9 @@ inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + kBlock - 1) / kBlo
 
 // the specialised tube step of the paper configuration (dtmpc_fast.hip)
 bool tube_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf);
-int64_t tube_fast_chunk(int N);
-size_t tube_fast_workspace_bytes(int N, int64_t B);
+// largest chunk (trajectories per launch) whose per-lane records fit one buffer resource at `lanes`
+int64_t tube_fast_chunk_max(int N, int lanes);
+size_t tube_fast_workspace_bytes(int N, int64_t B, int lanes, int64_t chunk);
 int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
                      const dtmpc_tube_state* S, const void* w, hipStream_t st);
 

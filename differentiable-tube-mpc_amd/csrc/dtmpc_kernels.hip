@@ -226,18 +226,17 @@ struct TubeArgs {
 };
 
 
-// LPT lanes per trajectory (1 or 2), chosen per launch (tube_lanes).  At the benchmark batch (65,536
-// trajectories) one lane per trajectory is exactly one wave per SIMD; two lanes (paired line search,
-// line_search_pair: each lane of a pair rolls out half the candidates, the rest of the step is
-// computed identically by both lanes and stored twice) measured 8.27 vs 7.54 ms there -- the
-// duplicated backward / commit work outweighs the overlap.  Below half the lane slots the machine
-// is mostly idle and the step is ONE wave's latency, which the paired line search cuts: there the
-// tube step uses two lanes.  DTMPC_TUBE_LANES=1|2 (environment) forces either, for the parity tests;
-// it is read by dtmpc_tube_lanes only, i.e. once, when the caller builds its state (state->lanes).
-// Two lanes while the paired waves still fit one per SIMD: 2 B <= (SIMDs x 64) lane slots of the
-// current device (MI355X: 256 CUs x 4 SIMDs x 64 = 65,536, i.e. B <= 32,768; measured at B = 32,768:
-// 3.63 ms paired vs 4.11 ms one lane, at B = 65,536 one lane wins).  Without a device (host-side
-// tests) the MI355X count is assumed.
+// Lanes per trajectory, chosen per batch when the caller builds its state (dtmpc_tube_lanes; the
+// generic kernel below takes LPT = 1 or 2, the f32 fast kernel 1, 2 or 4).  At the benchmark batch
+// (65,536 trajectories) one lane per trajectory is exactly one wave per SIMD; two lanes (paired line
+// search: each lane of a pair rolls out half the candidates, the rest of the step is computed
+// identically by both) measured 8.27 vs 7.54 ms there -- the duplicated work outweighs the overlap.
+// Below the lane slots the machine is mostly idle and the step is ONE wave's latency, which more lanes
+// per trajectory cut: 4 lanes while 4 B <= (SIMDs x 64) lane slots of the current device (MI355X: 256
+// CUs x 4 SIMDs x 64 = 65,536, i.e. B <= 16,384), 2 while 2 B <= slots (B <= 32,768).  The generic
+// kernel runs a 4-lane state with LPT = 2.  DTMPC_TUBE_LANES=1|2|4 (environment) forces a count, for
+// the parity tests; it is read by dtmpc_tube_lanes only, i.e. once, when the caller builds its state
+// (state->lanes).  Without a device (host-side tests) the MI355X count is assumed.
 static int64_t lane_slots() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -250,8 +249,9 @@ static int64_t lane_slots() {
 
 static int tube_lanes_default(int64_t B) {
   const char* e = getenv("DTMPC_TUBE_LANES");
-  if (e && (e[0] == '1' || e[0] == '2') && e[1] == 0) return e[0] - '0';
-  return 2 * B <= lane_slots() ? 2 : 1;
+  if (e && (e[0] == '1' || e[0] == '2' || e[0] == '4') && e[1] == 0) return e[0] - '0';
+  const int64_t slots = lane_slots();
+  return 4 * B <= slots ? 4 : 2 * B <= slots ? 2 : 1;
 }
 
 // One wave per SIMD is all either form gets (the two-lane form runs only at small batches), so the
@@ -467,7 +467,7 @@ static int launch_ilqr(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_i
 template <typename T>
 static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff,
                        int64_t step, const dtmpc_tube_state* S, const void* w, hipStream_t st) {
-  const int lpt = S->lanes;
+  const int lpt = S->lanes == 1 ? 1 : 2;  // a 4-lane state runs the generic kernel at two lanes
   DSpec<T> s = make_spec<T>(*sp);
   DCost<T> cn = make_cost<T>(cf->nominal);
   DIlqr<T> cfn = make_ilqr<T>(cf->nom_ilqr), cfa = make_ilqr<T>(cf->aux_ilqr);
@@ -510,6 +510,11 @@ static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B
     DTMPC_NA_CASES(CASE)
 #undef CASE
     default: return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
+  }
+  if (S->lanes > lpt) {  // the partial rows past the two-lane grid's: zero, so the reduction of all rows holds
+    const int64_t r0 = (B * lpt + kBlock - 1) / kBlock, r1 = (B * S->lanes + kBlock - 1) / kBlock;
+    if (r1 > r0 && hipMemsetAsync((T*)S->partials + r0 * DTMPC_TUBE_SUMS, 0, (size_t)(r1 - r0) * DTMPC_TUBE_SUMS * sizeof(T), st) != hipSuccess)
+      return check_launch("partials tail");
   }
   return check_launch("tube_step_kernel");
 }
@@ -681,19 +686,31 @@ int dtmpc_doc_grad(int dtype, int32_t horizon, int64_t B, const void* Xaux, cons
   return check_launch("docgrad_kernel");
 }
 
-size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
+int64_t dtmpc_tube_chunk(int32_t horizon, int32_t lanes) {
+  if (horizon < 1 || horizon > DTMPC_MAX_HORIZON || (lanes != 1 && lanes != 2 && lanes != 4)) return 0;
+  int64_t c = tube_fast_chunk_max(horizon, lanes);
+  if (const char* e = getenv("DTMPC_FAST_CHUNK")) {
+    const int64_t v = atoll(e) / kBlock * kBlock;
+    if (v > 0 && v < c) c = v;
+  }
+  return c;
+}
+
+size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t lanes, int64_t chunk) {
+  if (horizon < 1 || horizon > DTMPC_MAX_HORIZON || B < 1 || (lanes != 1 && lanes != 2 && lanes != 4)) return 0;
+  if (chunk < kBlock || chunk % kBlock || chunk > tube_fast_chunk_max(horizon, lanes)) return 0;
   size_t el = dtype == DTMPC_F64 ? 8 : 4;
   // generic kernel: sensitivity K / kf / AB (SoA, 20) + iLQR gains (AoS, 10) values per step;
   // the f32 fast kernel: its per-lane records for one chunk (dtmpc_fast.hip)
   const size_t gen = el * (size_t)horizon * 30 * (size_t)B;
-  const size_t fast = dtype == DTMPC_F32 ? tube_fast_workspace_bytes(horizon, B) : 0;
+  const size_t fast = dtype == DTMPC_F32 ? tube_fast_workspace_bytes(horizon, B, lanes, chunk) : 0;
   return gen > fast ? gen : fast;
 }
 
 int32_t dtmpc_tube_lanes(int64_t B) { return tube_lanes_default(B); }
 
 int64_t dtmpc_tube_partials_count(int64_t B, int32_t lanes) {
-  if (B < 1 || (lanes != 1 && lanes != 2)) return 0;
+  if (B < 1 || (lanes != 1 && lanes != 2 && lanes != 4)) return 0;
   return (B * lanes + kBlock - 1) / kBlock;
 }
 
@@ -714,9 +731,17 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
   if (!S->x || !S->b || !S->xbar || !S->bbar || !S->Xnom || !S->Unom || !S->Xaux || !S->Uaux ||
       !S->work || !S->theta || !S->partials || !S->status)
     return set_err(DTMPC_ERR_BAD_ARG, "NULL state array");
-  if (S->lanes != 1 && S->lanes != 2) return set_err(DTMPC_ERR_BAD_ARG, "state->lanes must be 1 or 2");
+  if (S->lanes != 1 && S->lanes != 2 && S->lanes != 4) return set_err(DTMPC_ERR_BAD_ARG, "state->lanes must be 1, 2 or 4");
   if (S->n_partials < dtmpc_tube_partials_count(B, S->lanes))
     return set_err(DTMPC_ERR_BAD_ARG, "state->n_partials < dtmpc_tube_partials_count(B, lanes)");
+  {
+    // the workspace the caller allocated must hold what this launch addresses (chunk and lanes come from
+    // the state, never from the environment)
+    const size_t need = dtmpc_tube_workspace_bytes(dtype, spec->horizon, B, S->lanes, S->chunk);
+    if (need == 0) return set_err(DTMPC_ERR_BAD_ARG, "state->chunk is not a chunk dtmpc_tube_chunk(horizon, lanes) returns");
+    if (S->work_bytes < 0 || (size_t)S->work_bytes < need)
+      return set_err(DTMPC_ERR_BAD_ARG, "state->work_bytes < dtmpc_tube_workspace_bytes(dtype, horizon, B, lanes, chunk)");
+  }
   if (cfg->disturbance == 0 && !w) return set_err(DTMPC_ERR_BAD_ARG, "injected disturbance w is NULL");
   if (cfg->disturbance != 0 && cfg->disturbance != 1) return set_err(DTMPC_ERR_BAD_ARG, "bad disturbance mode");
   hipStream_t st = (hipStream_t)stream;

@@ -616,7 +616,6 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
                          const Col<T>& X, const Col<T>& U, const G& gains,
                          const Col<T>& Xr, int rf, const Col<T>& Ur, int& iters, Prof& pr,
                          int pb, int h = 0) {
-  const int N = s.N;
   // V = clamp(V_init); X = rollout(x0, V)   (:127-131); the cost of that tape is the alpha = 0
   // candidate's cost (only needed when alpha = 0 is listed)
   T Jcur = init_tape(s, c, x0, X, U, Xr, rf, Ur, cfg.zpos >= 0 && cfg.max_iter > 0);

@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_OBS = 16
 MAX_ALPHAS = 8
 MAX_HORIZON = 512
@@ -24,6 +24,7 @@ BARRIER_INVERSE, BARRIER_LOG = 0, 1
 COST_TARGET, COST_TRACK = 0, 1
 OK, ERR_BAD_ARG, ERR_HIP = 0, 3, 4
 ST_NONFINITE, ST_NO_CANDIDATE = 1, 2
+BARRIER_INVERSE_PLAIN = 2  # include/dtmpc_systems.h: dtmpc_barrier_eval's plain 1 / max(z, eps)
 
 OBS_AGGREGATIONS = {"smoothmin": OBS_SMOOTHMIN, "min": OBS_MIN, "single": OBS_SINGLE, "none": OBS_NONE}
 BARRIERS = {"inverse": BARRIER_INVERSE, "log": BARRIER_LOG}
@@ -115,6 +116,8 @@ class DtmpcTubeState(C.Structure):
         ("lanes", C.c_int32),
         ("pad_", C.c_int32),
         ("n_partials", C.c_int64),
+        ("chunk", C.c_int64),
+        ("work_bytes", C.c_int64),
     ]
 
 
@@ -189,7 +192,8 @@ PROTOTYPES = {
         [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), I64, P, P, P, P, P, P, P, P, P, P, P],
     ),
     "dtmpc_doc_grad": (C.c_int, [C.c_int, I32, I64, P, P, P, P, P, P, P, P]),
-    "dtmpc_tube_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64]),
+    "dtmpc_tube_chunk": (I64, [I32, I32]),
+    "dtmpc_tube_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64, I32, I64]),
     "dtmpc_tube_lanes": (I32, [I64]),
     "dtmpc_tube_partials_count": (I64, [I64, I32]),
     "dtmpc_tube_step": (
@@ -220,6 +224,14 @@ PROTOTYPES = {
     "dtmpc_general_plant": (
         C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcGeneralCfg), I64, I64, I64,
                   C.POINTER(DtmpcGeneralState), P, P]),
+    # include/dtmpc_systems.h
+    "dtmpc_dubins_step": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), I64, I32, P, P, P, P]),
+    "dtmpc_h_eval": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), I64, I32, P, P, P, P]),
+    "dtmpc_barrier_eval": (C.c_int, [C.c_int, I32, C.c_double, C.c_double, I64, P, P, P, P]),
+    "dtmpc_fhat": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), I64, P, P, P, P]),
+    "dtmpc_aug_jac": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), I64, P, P, P, P, P]),
+    "dtmpc_box_clamp": (C.c_int, [C.c_int, C.POINTER(DtmpcSpec), I64, P, P, P, P]),
+    "dtmpc_cost_derivs": (C.c_int, [C.c_int, C.POINTER(DtmpcCost), I32, I64, P, P, P, P, P, P, P]),
     "dtmpc_receding_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64]),
     "dtmpc_nominal_receding": (
         C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, I32, C.c_double,

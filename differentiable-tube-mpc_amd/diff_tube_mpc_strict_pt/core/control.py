@@ -3,7 +3,8 @@
 * :class:`BoxClampControl` (core/control.py:38-70) -- the box the solvers clamp to.  Every solver
   entry point takes its bounds from the problem (``DubinsDBaSProblem.u_min / u_max / active_tol``);
   :meth:`BoxClampControl.problem_bounds` gives those fields, so a caller that builds the reference's
-  object keeps doing so.
+  object keeps doing so.  ``clamp`` and ``active_mask`` evaluate in the HIP kernel of
+  ``dtmpc_box_clamp`` (include/dtmpc_systems.h) over u [..., 2] on a HIP device.
 * :class:`BoxTanhControl` (core/control.py:10-35) -- u = u_min + (u_max - u_min)(tanh(v) + 1)/2 over an
   unconstrained decision variable v.  ``u`` and ``du_dv_diag`` evaluate in the HIP kernel of
   ``dtmpc_tanh_cost_derivs`` (include/dtmpc_control.h); v must be a device tensor of shape [..., 2].
@@ -44,6 +45,33 @@ class BoxClampControl:
         """Keyword arguments of :class:`DubinsDBaSProblem` for this box."""
         return {"u_min": _pair(self.u_min), "u_max": _pair(self.u_max), "active_tol": float(self.active_tol)}
 
+    def _eval(self, u: Tensor, want_u: bool, want_mask: bool):
+        from . import _points as P
+
+        P.require_device(u)
+        unbatched = u.ndim == 1
+        us = u.unsqueeze(0) if unbatched else u
+        ur, lead = P.rows(us, 2, us)
+        n = ur.shape[0]
+        uo = torch.empty_like(ur) if want_u else None
+        m = torch.empty(n, 2, dtype=torch.bool, device=ur.device) if want_mask else None
+        if n > 0:
+            b = self.problem_bounds()
+            sp = P.spec(u_min=b["u_min"], u_max=b["u_max"], active_tol=b["active_tol"])
+            P.launch("dtmpc_box_clamp", P.dtype_code(ur), P.byref(sp), n, ur.data_ptr(), P.ptr(uo), P.ptr(m),
+                     P.stream(ur))
+        out = uo if want_u else m
+        out = out.reshape(*lead, 2)
+        return out.squeeze(0) if unbatched else out
+
+    def clamp(self, u: Tensor) -> Tensor:
+        """core/control.py:61-64: torch.clamp(u, u_min, u_max) (NaN propagates)."""
+        return self._eval(u, True, False)
+
+    def active_mask(self, u: Tensor) -> Tensor:
+        """core/control.py:66-70: bool [..., 2], u within active_tol of a bound."""
+        return self._eval(u, False, True)
+
 
 @dataclass(frozen=True)
 class BoxTanhControl:
@@ -53,9 +81,7 @@ class BoxTanhControl:
     u_max: Sequence[float] | Tensor
 
     def __post_init__(self) -> None:
-        lo, hi = _pair(self.u_min), _pair(self.u_max)
-        if not all(h > l for l, h in zip(lo, hi)):
-            raise ValueError("u_max must exceed u_min")
+        _pair(self.u_min), _pair(self.u_max)  # two bounds per side (any values, as the reference)
 
     def problem(self, horizon: int = 1) -> DubinsDBaSProblem:
         return DubinsDBaSProblem(horizon=horizon, u_min=_pair(self.u_min), u_max=_pair(self.u_max))

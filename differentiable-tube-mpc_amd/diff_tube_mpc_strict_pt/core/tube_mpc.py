@@ -136,10 +136,14 @@ class TubeMPC:
         self.Unom = torch.zeros(N, 2, B, **kw)
         self.Xaux = torch.zeros(N + 1, 4, B, **kw)
         self.Uaux = torch.zeros(N, 2, B, **kw)
-        self.work = torch.empty(self.lib.dtmpc_tube_workspace_bytes(self._dt, N, B), dtype=torch.uint8,
-                                device=self.device)
-        # lanes per trajectory: resolved once here (DTMPC_TUBE_LANES is read by the library only now)
+        # lanes per trajectory and the fast kernel's launch chunk: resolved once here (DTMPC_TUBE_LANES and
+        # DTMPC_FAST_CHUNK are read by the library only now), and the workspace sized for exactly these
         self.lanes = int(self.lib.dtmpc_tube_lanes(B))
+        self.chunk = int(self.lib.dtmpc_tube_chunk(N, self.lanes))
+        wbytes = int(self.lib.dtmpc_tube_workspace_bytes(self._dt, N, B, self.lanes, self.chunk))
+        if wbytes <= 0:
+            raise ValueError(f"no tube-step workspace for horizon {N}, batch {B}, lanes {self.lanes}")
+        self.work = torch.empty(wbytes, dtype=torch.uint8, device=self.device)
         self.n_partials = int(self.lib.dtmpc_tube_partials_count(B, self.lanes))
         self.partials = torch.zeros(self.n_partials, _abi.TUBE_SUMS, **kw)
         self.sums = torch.zeros(_abi.TUBE_SUMS, **kw)
@@ -161,6 +165,8 @@ class TubeMPC:
         st.iters = self.iters.data_ptr()
         st.lanes = self.lanes
         st.n_partials = self.n_partials
+        st.chunk = self.chunk
+        st.work_bytes = wbytes
         self.state = st
 
     # -----------------------------------------------------------------------------------------

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DTMPC_ABI_VERSION 3
+#define DTMPC_ABI_VERSION 4
 #define DTMPC_MAX_OBS 16
 #define DTMPC_MAX_ALPHAS 8
 #define DTMPC_MAX_HORIZON 512
@@ -165,6 +165,10 @@ typedef struct dtmpc_tube_state {
   int32_t lanes;    /* lanes per trajectory, fixed when the state is built: dtmpc_tube_lanes(B) */
   int32_t pad_;
   int64_t n_partials; /* rows of `partials`; must be >= dtmpc_tube_partials_count(B, lanes) */
+  int64_t chunk;    /* trajectories per launch of the f32 fast kernel, fixed when the state is built:
+                       dtmpc_tube_chunk(horizon, lanes) */
+  int64_t work_bytes; /* size of `work`; must be >=
+                         dtmpc_tube_workspace_bytes(dtype, horizon, B, lanes, chunk) */
 } dtmpc_tube_state;
 
 int dtmpc_abi_version(void);
@@ -232,12 +236,20 @@ int dtmpc_doc_grad(int dtype, int32_t horizon, int64_t B, const void* Xaux, cons
 
 /* ---- fused closed-loop step (Algorithm 2 body) ----------------------------------------- */
 
-/* Scratch bytes for dtmpc_tube_step. */
-size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B);
-/* Lanes per trajectory the fused step uses for a batch of B: 1 above 16,384 trajectories (one wave
- * per SIMD at the benchmark batch), 2 below (paired line search); the environment variable
- * DTMPC_TUBE_LANES=1|2 overrides.  Resolved ONCE, when the caller builds its state
- * (dtmpc_tube_state.lanes); dtmpc_tube_step never reads the environment. */
+/* Trajectories per launch of the f32 fast kernel: its per-lane workspace records stay below 2^31 bytes
+ * (one buffer resource); the environment variable DTMPC_FAST_CHUNK (a smaller chunk, for the tests of
+ * the chunked launch) is read here only.  Resolved ONCE, when the caller builds its state
+ * (dtmpc_tube_state.chunk); dtmpc_tube_step never reads it. */
+int64_t dtmpc_tube_chunk(int32_t horizon, int32_t lanes);
+/* Scratch bytes for dtmpc_tube_step at `lanes` lanes per trajectory and `chunk` (dtmpc_tube_chunk).
+ * 0 if lanes is not a supported count or chunk is not one dtmpc_tube_chunk can return. */
+size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t lanes, int64_t chunk);
+/* Lanes per trajectory the fused step uses for a batch of B on the current device (lane slots =
+ * CUs x 4 SIMDs x 64, 65,536 on MI355X): 4 while 4 B <= slots (B <= 16,384: one line-search pair per
+ * lane, candidate tapes kept instead of a commit pass), 2 while 2 B <= slots (paired line search),
+ * else 1 (one wave per SIMD at the benchmark batch); the environment variable DTMPC_TUBE_LANES=1|2|4
+ * overrides.  Resolved ONCE, when the caller builds its state (dtmpc_tube_state.lanes);
+ * dtmpc_tube_step never reads the environment. */
 int32_t dtmpc_tube_lanes(int64_t B);
 /* Number of per-workgroup partial records dtmpc_tube_step writes for B trajectories at `lanes`
  * lanes per trajectory (0 if lanes is not a supported count). */

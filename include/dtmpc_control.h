@@ -18,7 +18,8 @@ extern "C" {
  *   replaces core/control.py:10-35 `BoxTanhControl.u` / `du_dv_diag`, core/cost_derivs.py:16-24
  *   `_d2u_dv2_diag`, core/cost_derivs.py:27-55 `nominal_cost_derivs` (cost->kind TARGET) and
  *   core/cost_derivs.py:79-107 `auxiliary_cost_derivs` (cost->kind TRACK).
- *   Box bounds: spec->u_min / u_max (u_max > u_min).  cost->wrap_angle must be 0.
+ *   Box bounds: spec->u_min / u_max (any values, as the reference's map takes them).  cost->wrap_angle
+ *   must be 0.
  *   X [N+1][4][B] (rows 0..N-1 read; may be NULL when lx is NULL), Vdec [N][2][B]; Xref [N+1][3][B] / Uref [N][2][B] read only
  *   for TRACK.  Outputs (each may be NULL): U [N][2][B] = u(v), dU [N][2][B] = du/dv,
  *   lx [N][4][B] = l_x, lv [N][2][B] = l_v, lvv [N][2][B] = diag(l_vv).  l_xx = diag(2Q, 2qb) and

@@ -460,10 +460,12 @@ static REAL FN(traj_cost)(const SPEC_T* s, const COST_T* c, const REAL* X, const
 
 /* ---- iLQR (core/ddp.py:102-307) ------------------------------------------------------------ */
 
-/* work: >= (2*(N+1)*4 + 2*2*N) REALs. Returns status bits; *iters = iterations run. */
+/* work: >= (2*(N+1)*4 + 2*2*N) REALs. Returns status bits; *iters = iterations run.  choice (or NULL):
+ * the line search's winning alpha position of iteration it at choice[it * cstride] (the decision record
+ * of SURVEY.md §8c; iterations not run are left as the caller set them). */
 static int FN(ilqr1)(const SPEC_T* s, const COST_T* c, const dtmpc_ilqr_cfg* cfg, const REAL* x0,
                      const REAL* Xr, const REAL* Ur, REAL* X, REAL* V, REAL* K, REAL* kff,
-                     int* iters, REAL* work) {
+                     int* iters, REAL* work, signed char* choice, long long cstride) {
   int N = s->N;
   REAL reg = (REAL)cfg->reg, tol = (REAL)cfg->tol;
   REAL* Xc = work;
@@ -517,7 +519,7 @@ static int FN(ilqr1)(const SPEC_T* s, const COST_T* c, const dtmpc_ilqr_cfg* cfg
         return DTMPC_ST_NONFINITE;
     }
     /* forward pass with line search :256-301 */
-    int have_best = 0;
+    int have_best = 0, best_ia = -1;
     REAL best = 0;
     for (int ia = 0; ia < cfg->n_alphas; ++ia) {
       REAL al = (REAL)cfg->alphas[ia];
@@ -544,11 +546,13 @@ static int FN(ilqr1)(const SPEC_T* s, const COST_T* c, const dtmpc_ilqr_cfg* cfg
       if (!have_best || J < best) {
         have_best = 1;
         best = J;
+        best_ia = ia;
         memcpy(Xb, Xc, sizeof(REAL) * 4 * (N + 1));
         memcpy(Vb, Vc, sizeof(REAL) * 2 * N);
       }
     }
     if (!have_best) return DTMPC_ST_NO_CANDIDATE;
+    if (choice) choice[(long long)it * cstride] = (signed char)best_ia;
     memcpy(X, Xb, sizeof(REAL) * 4 * (N + 1));
     memcpy(V, Vb, sizeof(REAL) * 2 * N);
     /* :303-305 */
@@ -869,10 +873,11 @@ void FN(oracle_linearize)(const dtmpc_spec* sp, const dtmpc_cost* cp, long long 
   }
 }
 
-void FN(oracle_ilqr_solve)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cfg,
-                           long long B, const REAL* x0, const REAL* Xref, const REAL* Uref,
-                           REAL* X, REAL* U, REAL* K, REAL* kff, int* iters, int* status,
-                           int nthreads) {
+/* choices (or NULL): [max_iter][B] winning alpha position per iteration, -1 where none ran */
+void FN(oracle_ilqr_solve_ex)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cfg,
+                              long long B, const REAL* x0, const REAL* Xref, const REAL* Uref,
+                              REAL* X, REAL* U, REAL* K, REAL* kff, int* iters, int* status,
+                              signed char* choices, int nthreads) {
   SPEC_T s;
   COST_T c;
   FN(spec_from)(sp, &s);
@@ -903,8 +908,11 @@ void FN(oracle_ilqr_solve)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtm
       memset(Ka, 0, sizeof(REAL) * 8 * N);
       memset(ka, 0, sizeof(REAL) * 2 * N);
       int it = 0;
+      if (choices)
+        for (int j = 0; j < cfg->max_iter; ++j) choices[(long long)j * B + i] = -1;
       int st = FN(ilqr1)(&s, &c, cfg, x0a, c.kind == DTMPC_COST_TRACK ? Xr : NULL,
-                         c.kind == DTMPC_COST_TRACK ? Ur : NULL, Xa, Va, Ka, ka, &it, wk);
+                         c.kind == DTMPC_COST_TRACK ? Ur : NULL, Xa, Va, Ka, ka, &it, wk,
+                         choices ? choices + i : NULL, B);
       FN(scatter)(Xa, N + 1, 4, B, i, X);
       FN(scatter)(Va, N, 2, B, i, U);
       if (K) FN(scatter)(Ka, N, 8, B, i, K);
@@ -980,11 +988,13 @@ void FN(oracle_doc_grad)(int N, long long B, const REAL* Xa, const REAL* Ua, con
 /* Algorithm-2 loop body per trajectory (core/tube_mpc.py:813-1023), theta read-only.
  * State arrays SoA as dtmpc_tube_state (host memory).  gout [7][B] per-trajectory L, gQ, gR, gqb.
  * log [18][B] (may be NULL).  w [3][B] (may be NULL when cfg->disturbance == 1). */
-void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long long B,
-                          long long goff, long long step, REAL* x, REAL* b, REAL* xbar,
-                          REAL* bbar, REAL* Xnom, REAL* Unom, REAL* Xaux, REAL* Uaux,
-                          const REAL* theta, const REAL* w, REAL* gout, REAL* log, int* status,
-                          int* iters, int nthreads) {
+/* choices (or NULL): [nom max_iter + aux max_iter][B] winning alpha position per iteration of the
+ * nominal, then the ancillary solve, -1 where none ran */
+void FN(oracle_tube_step_ex)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long long B,
+                             long long goff, long long step, REAL* x, REAL* b, REAL* xbar,
+                             REAL* bbar, REAL* Xnom, REAL* Unom, REAL* Xaux, REAL* Uaux,
+                             const REAL* theta, const REAL* w, REAL* gout, REAL* log, int* status,
+                             int* iters, signed char* choices, int nthreads) {
   SPEC_T s;
   COST_T cn, ca;
   FN(spec_from)(sp, &s);
@@ -1030,13 +1040,17 @@ void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long 
       /* nominal solve from [xbar, bbar] :813-857 */
       x0[0] = xb[0]; x0[1] = xb[1]; x0[2] = xb[2]; x0[3] = bb;
       FN(gather)(Unom, N, 2, B, i, Vn);
-      st |= FN(ilqr1)(&s, &cn, &cfg->nom_ilqr, x0, NULL, NULL, Xn, Vn, Ka, ka, &itn, wk);
+      if (choices)
+        for (int j = 0; j < cfg->nom_ilqr.max_iter + cfg->aux_ilqr.max_iter; ++j) choices[(long long)j * B + i] = -1;
+      st |= FN(ilqr1)(&s, &cn, &cfg->nom_ilqr, x0, NULL, NULL, Xn, Vn, Ka, ka, &itn, wk,
+                      choices ? choices + i : NULL, B);
       /* ancillary solve tracking the nominal :863-909 */
       for (int k = 0; k <= N; ++k)
         for (int f = 0; f < 3; ++f) Xr[3 * k + f] = Xn[4 * k + f];
       x0[0] = xs[0]; x0[1] = xs[1]; x0[2] = xs[2]; x0[3] = bs;
       FN(gather)(Uaux, N, 2, B, i, Va);
-      st |= FN(ilqr1)(&s, &ca, &cfg->aux_ilqr, x0, Xr, Vn, Xa, Va, Ka, ka, &ita, wk);
+      st |= FN(ilqr1)(&s, &ca, &cfg->aux_ilqr, x0, Xr, Vn, Xa, Va, Ka, ka, &ita, wk,
+                      choices ? choices + (long long)cfg->nom_ilqr.max_iter * B + i : NULL, B);
       /* sensitivity + DOC gradient :915-976 */
       st |= FN(sens1)(&s, &ca, Xa, Va, Xr, Vn, Xr, NULL, NULL, dXa, dVa, NULL, wk2);
       REAL o[7];
@@ -1088,6 +1102,22 @@ void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long 
     }
     free(buf);
   }
+}
+
+void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long long B,
+                          long long goff, long long step, REAL* x, REAL* b, REAL* xbar,
+                          REAL* bbar, REAL* Xnom, REAL* Unom, REAL* Xaux, REAL* Uaux,
+                          const REAL* theta, const REAL* w, REAL* gout, REAL* log, int* status,
+                          int* iters, int nthreads) {
+  FN(oracle_tube_step_ex)(sp, cfg, B, goff, step, x, b, xbar, bbar, Xnom, Unom, Xaux, Uaux, theta, w, gout, log,
+                          status, iters, NULL, nthreads);
+}
+
+void FN(oracle_ilqr_solve)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cfg,
+                           long long B, const REAL* x0, const REAL* Xref, const REAL* Uref,
+                           REAL* X, REAL* U, REAL* K, REAL* kff, int* iters, int* status,
+                           int nthreads) {
+  FN(oracle_ilqr_solve_ex)(sp, cp, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, NULL, nthreads);
 }
 
 /* momentum + projected update core/tube_mpc.py:978-984 with g = sums[1:7] * inv_batch, or for

@@ -117,16 +117,28 @@ def test_arguments_validated_before_any_device_call(lib):
     rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
     assert rc == _abi.ERR_BAD_ARG and b"same width" in lib.dtmpc_last_error()
     # f32: the larger of the generic kernel's scratch (30 values per step) and the fast kernel's per-lane
-    # records (two tapes of (N+1) x 16 B + N x 8 B, gains and sensitivity scratch of N x 40 B per trajectory)
-    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536) == max(4 * 50 * 30, 51 * 32 + 50 * 96) * 65536
-    assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 65536) == 8 * 50 * 30 * 65536
+    # records (two tapes of (N+1) x 16 B + N x 8 B, gains and sensitivity scratch of N x 40 B per
+    # trajectory; four lanes: twelve tape slots per solve), for one launch chunk
+    per1, per4 = 51 * 32 + 50 * 96, 12 * (51 * 32 + 50 * 16) + 50 * 80
+    c1, c4 = lib.dtmpc_tube_chunk(50, 1), lib.dtmpc_tube_chunk(50, 4)
+    assert c1 == (0x7FFFFFFF // per1) // 256 * 256 and c4 == (0x7FFFFFFF // per4) // 256 * 256
+    assert lib.dtmpc_tube_chunk(50, 3) == 0
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536, 1, c1) == max(4 * 50 * 30, per1) * 65536
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 4096, 4, c4) == per4 * 4096
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 65536, 1, c1) == 8 * 50 * 30 * 65536
     # above 2^31 bytes of records the fast kernel runs in chunks: the workspace holds one chunk
-    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 1 << 22) == 4 * 50 * 30 * (1 << 22)
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 1 << 22, 1, c1) == 4 * 50 * 30 * (1 << 22)
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 100000, 4, c4) == per4 * c4
+    # a chunk no dtmpc_tube_chunk returns (too large, not a workgroup multiple) or a bad lane count: 0
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536, 4, c1) == 0
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536, 1, 1000) == 0
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536, 3, c1) == 0
     assert lib.dtmpc_tube_partials_count(65536, 1) == 256
     assert lib.dtmpc_tube_partials_count(1000, 2) == 8
     assert lib.dtmpc_tube_partials_count(1000, 3) == 0
     assert lib.dtmpc_general_partials_count(1000) == 4
-    assert lib.dtmpc_tube_lanes(65536) in (1, 2) and lib.dtmpc_tube_lanes(4096) in (1, 2)
+    assert lib.dtmpc_tube_partials_count(1000, 4) == 16
+    assert lib.dtmpc_tube_lanes(65536) in (1, 2, 4) and lib.dtmpc_tube_lanes(4096) in (1, 2, 4)
     # the lane count and the partials size come from the state (resolved once by the caller)
     tc.aux_ilqr = st.ilqr_aux.to_c()
     for f in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux", "work", "theta", "partials", "status"):
@@ -137,6 +149,16 @@ def test_arguments_validated_before_any_device_call(lib):
     state.lanes, state.n_partials = 2, 0
     rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
     assert rc == _abi.ERR_BAD_ARG and b"n_partials" in lib.dtmpc_last_error()
+    # the chunk and the workspace size come from the state and are checked against each other (a chunk
+    # changed after the workspace was sized cannot make the kernel address past it)
+    state.n_partials = lib.dtmpc_tube_partials_count(8, 2)
+    state.chunk, state.work_bytes = 300, 1 << 30
+    rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
+    assert rc == _abi.ERR_BAD_ARG and b"chunk" in lib.dtmpc_last_error()
+    state.chunk = lib.dtmpc_tube_chunk(50, 2)
+    state.work_bytes = lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 8, 2, state.chunk) - 1
+    rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
+    assert rc == _abi.ERR_BAD_ARG and b"work_bytes" in lib.dtmpc_last_error()
     assert lib.dtmpc_sensitivity_workspace_bytes(_abi.F64, 50, 10, 1) == 8 * 10 * (50 * 20 + 51 * 20)
     # the fused episode reset validates before launching
     rc = lib.dtmpc_tube_reset(_abi.F32, C.byref(spec), 8, None, C.byref(state), 1, 1, 1, None)

@@ -59,10 +59,6 @@ def test_tanh_abi_arguments_validated(oracle_lib):
     assert rc == _abi.ERR_BAD_ARG and b"unwrapped" in lib.dtmpc_last_error()
     rc = lib.dtmpc_tanh_cost_derivs(_abi.F64, C.byref(sp), C.byref(cn), 4, None, 1, None, None, 1, 1, 1, 1, 1, None)
     assert rc == _abi.ERR_BAD_ARG and b"NULL" in lib.dtmpc_last_error()
-    flat = tanh_case("f64")[1]
-    flat.u_max[1] = flat.u_min[1]
-    rc = lib.dtmpc_tanh_cost_derivs(_abi.F64, C.byref(flat), C.byref(cn), 4, 1, 1, None, None, 1, 1, 1, 1, 1, None)
-    assert rc == _abi.ERR_BAD_ARG and b"u_max" in lib.dtmpc_last_error()
     rc = lib.dtmpc_tanh_cost_derivs(_abi.F64, C.byref(sp), C.byref(cn), 0, 1, 1, None, None, 1, 1, 1, 1, 1, None)
     assert rc == _abi.ERR_BAD_ARG and b"batch" in lib.dtmpc_last_error()
     rc = lib.dtmpc_tanh_cost_derivs(7, C.byref(sp), C.byref(cn), 4, 1, 1, None, None, 1, 1, 1, 1, 1, None)
@@ -75,8 +71,10 @@ def test_box_controls_host_side():
     b = BoxClampControl(u_min=(-10.0, -np.pi), u_max=(10.0, np.pi))
     p = DubinsDBaSProblem(**b.problem_bounds())
     assert p.u_max == (10.0, np.pi) and p.active_tol == 1e-8
+    # any bounds, as the reference's map takes them (core/control.py:10-35 has no ordering check)
+    BoxTanhControl(u_min=(1.0, 0.0), u_max=(1.0, 1.0))
     with pytest.raises(ValueError):
-        BoxTanhControl(u_min=(1.0, 0.0), u_max=(1.0, 1.0))
+        BoxTanhControl(u_min=(1.0, 0.0, 2.0), u_max=(1.0, 1.0))
 
 
 def test_tanh_mirror_refuses_host_tensors():
