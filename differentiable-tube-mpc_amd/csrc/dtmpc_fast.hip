@@ -83,6 +83,8 @@ struct FArgs {
   unsigned long long seed;
   float wlo[3], whi[3];
   int stagger;  // s_sleep(127) rounds before this workgroup starts (phase desynchronisation, see launch)
+  signed char* choices;  // [nom max_iter + aux max_iter][B] or NULL (dtmpc_tube_state.choices)
+  float gbound;          // health bound on the gradient row (dtmpc_tube_cfg.grad_bound; +inf: none)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -193,14 +195,17 @@ __device__ __forceinline__ void rst2(Rsrc, const RA& a, int k, unsigned off, f2 
 }
 #endif
 
-// LDS-resident gains.  The iLQR gains of the first KL steps of the horizon live in the LDS of the
-// trajectory's CU instead of the workspace: the backward pass writes them, the line search and the
-// commit read them (core/ddp.py:248-249, 266-269) -- three HBM passes over 32 B per step and iteration
-// that never leave the CU.  One workgroup per CU holds all 160 KiB: quad q (16 B) of step s of the
-// trajectory with workgroup-local index j is at lds[(s * Q + q) * LS + j] (LS = trajectories per
-// workgroup), so a wave's access is 64 consecutive 16-B slots (conflict-free ds_read/write_b128) and the
-// lanes of one trajectory (P > 1) read one address (broadcast).  KL = what fits: 20 steps at one lane per
-// trajectory (gamma = 0 records), 40 at two, the whole horizon at four.
+// LDS-resident gains (compile-time option, OFF by default: -D DTMPC_FAST_LDS_STEPS=n keeps the iLQR gains
+// of the first n steps in the LDS of the trajectory's CU instead of the workspace).  The backward pass
+// would write them there and the line search and the commit read them (core/ddp.py:248-249, 266-269):
+// three HBM passes over 32 B per step and iteration that never leave the CU.  Layout: one workgroup per
+// CU holds all 160 KiB; quad q (16 B) of step s of the trajectory with workgroup-local index j is at
+// lds[(s * Q + q) * LS + j] (LS = trajectories per workgroup), a wave's access 64 consecutive 16-B slots
+// (conflict-free ds_read/write_b128), the lanes of one trajectory reading one address (broadcast).
+// Measured and rejected (round 3, same-box A/B, profiles/r03/ab_lds.txt): 20 steps at one lane per
+// trajectory 4.05 -> 4.12 ms at B = 65,536, the whole horizon at four lanes 2.21 -> 2.52 ms at B = 4,096
+// -- the step is issue- and latency-bound, not HBM-bound, and a ds_write_b128 costs a wave ~13-26 issue
+// cycles against a buffer store's few; the bytes saved do not buy time.
 typedef __attribute__((address_space(3))) f4 lf4;
 constexpr int kLdsF4 = 163840 / 16;  // 160 KiB: the whole LDS of a CU, one workgroup per CU
 
@@ -208,15 +213,14 @@ template <int P, bool G0>
 struct GainLds {
   static constexpr int Q = G0 ? 2 : 3;          // 16-byte quads per step: K (2) [+ k]
   static constexpr int LS = kBlock / P;         // trajectories per workgroup
-  // steps held in LDS.  Only the gamma = 0 records (the paper's and the benchmark's DBaS) use it: with the
-  // general 40-byte records in three quads per step the results differed from the workspace-only path in
-  // a same-box diagnostic (scripts/diag_g0.py; deterministic, cause not found), so they stay in the
-  // workspace.
-#ifdef DTMPC_FAST_LDS_STEPS  // A/B and diagnostics: at most this many steps in LDS (0: none)
-  static constexpr int KL = !G0 ? 0 : kLdsF4 / (LS * Q) < DTMPC_FAST_LDS_STEPS ? kLdsF4 / (LS * Q) : DTMPC_FAST_LDS_STEPS;
-#else
-  static constexpr int KL = !G0 ? 0 : kLdsF4 / (LS * Q);
+  // steps held in LDS (at most what fits).  Only the gamma = 0 records: with the general 40-byte records
+  // in three quads per step the results differed from the workspace-only path in a same-box diagnostic
+  // (scripts/diag_g0.py; deterministic, cause not found), so those always stay in the workspace.
+#ifndef DTMPC_FAST_LDS_STEPS
+#define DTMPC_FAST_LDS_STEPS 0
 #endif
+  static constexpr int KL = !G0 ? 0 : kLdsF4 / (LS * Q) < DTMPC_FAST_LDS_STEPS ? kLdsF4 / (LS * Q) : DTMPC_FAST_LDS_STEPS;
+  static constexpr bool used = KL > 0;
 };
 
 template <int P>
@@ -1511,8 +1515,11 @@ constexpr int kSlotInit = 6;   // the initial rollout: bank 1, so the first line
 // kept every candidate's tape (Slots) and the winner's slot becomes the current tape (S.XA / S.UA).
 template <bool TRACK, int M, int P, class SV>
 __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const float* x0,
-                                    SV& S, int h, const SlotMap& sm, int& iters, Prof& pf) {
+                                    SV& S, int h, const SlotMap& sm, int& iters, Prof& pf, signed char* ch,
+                                    size_t chs) {
   constexpr int ph = TRACK ? 4 : 0;  // phase-timer slots (profiling builds)
+  if (ch && h == 0)  // the decision record: -1 for iterations not run (dtmpc_tube_state.choices)
+    for (int it = 0; it < cf.max_iter; ++it) ch[it * chs] = -1;
   float Jcur = init_tape<TRACK, M>(p, c, x0, S, cf.zpos >= 0 && cf.max_iter > 0);
   const float Bc0 = barrier_at<M>(p, x0[0], x0[1]);
   bool have_prev = false;
@@ -1548,6 +1555,7 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
       st = DTMPC_ST_NONFINITE;
       break;
     }
+    if (ch && h == 0) ch[it * chs] = (signed char)best;
     if (al != 0.f) {
       if (P == 4) {
         cur = nb + bc;
@@ -1793,7 +1801,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 
 tube_fast_kernel(FK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
   (void)kk;  // read through kargs()
-  __shared__ f4 lds[kLdsF4];  // the gains of the first steps (Gains); the workgroup sums at the end
+  // the gains of the first steps when DTMPC_FAST_LDS_STEPS > 0 (Gains); the workgroup sums at the end
+  __shared__ f4 lds[DTMPC_FAST_LDS_STEPS > 0 ? kLdsF4 : kBlock / 64 * DTMPC_TUBE_SUMS / 4];
   const int B = kargs()->a.B, Bc = kargs()->a.Bc, i0 = kargs()->a.i0;
   const int gl = blockIdx.x * kBlock + threadIdx.x;
   const int t = gl / P, h = gl % P;  // t: index in the chunk, h: lane of the trajectory
@@ -1852,7 +1861,8 @@ tube_fast_kernel(FK kk) {
       const FCost cn = K->cn;
       const FIlqr cfn = K->cfn;
       const float xn0[4] = {y0, y1, y2, yb};
-      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, sm, itn, pf);
+      signed char* ch = K->a.choices ? K->a.choices + i : nullptr;
+      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, sm, itn, pf, ch, nb);
     }
     FCost ca;  // ancillary weights theta (shared by the batch), terminal weight Qa (:885, :891)
     {
@@ -1881,7 +1891,8 @@ tube_fast_kernel(FK kk) {
       const FP p = phase_p<M>();
       const FIlqr cfa = K->cfa;
       const float xa0[4] = {x0, x1, x2, xb};
-      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, sm, ita, pf);
+      signed char* ch = K->a.choices ? K->a.choices + (size_t)K->cfn.max_iter * nb + i : nullptr;
+      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, sm, ita, pf, ch, nb);
     }
     pf.mark(8);
     {  // upper loss, DOC sensitivity and gradient (:915-976)
@@ -1946,7 +1957,12 @@ tube_fast_kernel(FK kk) {
         a.bbar[i] = qb;
       }
       acc[7] = 1.f;
-      if (st || h != 0) {  // healthy trajectories only; a trajectory's lanes count once
+      // healthy trajectories only (status 0 and every gradient component within the bound, NaN failing
+      // the test); a trajectory's lanes count once
+      float gm = m_abs(acc[1]);
+#pragma unroll
+      for (int j = 2; j < 7; ++j) gm = vmaxnan(gm, m_abs(acc[j]));
+      if (st || h != 0 || !(gm <= a.gbound)) {
 #pragma unroll
         for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) acc[j] = 0.f;
       }
@@ -2103,6 +2119,8 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
   a.status = S->status;
   a.iters = S->iters;
   a.w = (const float*)w;
+  a.choices = (signed char*)S->choices;
+  a.gbound = cf->grad_bound > 0 ? float(cf->grad_bound) : __builtin_inff();
   a.disturbance = cf->disturbance;
   a.write_log = (cf->write_log && S->log) ? 1 : 0;
   a.seed = cf->seed;

@@ -125,7 +125,8 @@ template <typename T, int NA>
 __global__ void __launch_bounds__(kBlock) ilqr_kernel(DSpec<T> s, DCost<T> c, DIlqr<T> cfg, int B,
                                                       const void* x0p, const void* Xrp,
                                                       const void* Urp, void* Xp, void* Up,
-                                                      void* Kp, void* kfp, int* iters, int* status) {
+                                                      void* Kp, void* kfp, int* iters, int* status,
+                                                      signed char* choices) {
   int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= B) return;
   Col<T> cx0 = col<T>(x0p, i, B);
@@ -135,7 +136,7 @@ __global__ void __launch_bounds__(kBlock) ilqr_kernel(DSpec<T> s, DCost<T> c, DI
   pr.start();
   int st = ilqr_traj<T, NA>(s, c, cfg, x0, col<T>(Xp, i, B), col<T>(Up, i, B),
                             GainsSoA<T>{col<T>(Kp, i, B), col<T>(kfp, i, B)}, col<T>(Xrp, i, B), 3,
-                            col<T>(Urp, i, B), it, pr, 0);
+                            col<T>(Urp, i, B), it, pr, 0, 0, choices ? choices + i : nullptr, (size_t)B);
   pr.flush();
   if (iters) iters[i] = it;
   if (status) status[i] |= st;
@@ -223,6 +224,8 @@ struct TubeArgs {
   int disturbance, write_log;
   uint64_t seed;
   T wlo[3], whi[3];
+  signed char* choices;  // [nom max_iter + aux max_iter][B] or NULL
+  T gbound;              // health bound on the gradient row (+inf: none)
 };
 
 
@@ -232,8 +235,10 @@ struct TubeArgs {
 // search: each lane of a pair rolls out half the candidates, the rest of the step is computed
 // identically by both) measured 8.27 vs 7.54 ms there -- the duplicated work outweighs the overlap.
 // Below the lane slots the machine is mostly idle and the step is ONE wave's latency, which more lanes
-// per trajectory cut: 4 lanes while 4 B <= (SIMDs x 64) lane slots of the current device (MI355X: 256
-// CUs x 4 SIMDs x 64 = 65,536, i.e. B <= 16,384), 2 while 2 B <= slots (B <= 32,768).  The generic
+// per trajectory cut: 4 lanes while 8 B <= (SIMDs x 64) lane slots of the current device (MI355X: 256
+// CUs x 4 SIMDs x 64 = 65,536, i.e. B <= 8,192: measured 2.22 / 2.30 ms at B = 4,096 / 8,192 against
+// 2.92 / 2.93 at two lanes; at B = 16,384 four lanes fill every SIMD with duplicated backward work and
+// lose, 3.76 vs 3.06 ms), 2 while 2 B <= slots (B <= 32,768).  The generic
 // kernel runs a 4-lane state with LPT = 2.  DTMPC_TUBE_LANES=1|2|4 (environment) forces a count, for
 // the parity tests; it is read by dtmpc_tube_lanes only, i.e. once, when the caller builds its state
 // (state->lanes).  Without a device (host-side tests) the MI355X count is assumed.
@@ -251,7 +256,7 @@ static int tube_lanes_default(int64_t B) {
   const char* e = getenv("DTMPC_TUBE_LANES");
   if (e && (e[0] == '1' || e[0] == '2' || e[0] == '4') && e[1] == 0) return e[0] - '0';
   const int64_t slots = lane_slots();
-  return 4 * B <= slots ? 4 : 2 * B <= slots ? 2 : 1;
+  return 8 * B <= slots ? 4 : 2 * B <= slots ? 2 : 1;
 }
 
 // One wave per SIMD is all either form gets (the two-lane form runs only at small batches), so the
@@ -288,7 +293,8 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
     // SoA cells of other lanes, which other waves may be writing in their sensitivity pass meanwhile.
     const GainsAoS<T> gains{a.work + (size_t)N * 20 * nb, a.work + (size_t)N * 28 * nb, (unsigned)B,
                             (unsigned)i};
-    st |= ilqr_traj<T, NA, LPT>(s, cn, cfn, xn0, Xn, Un, gains, none, 0, none, itn, pr, 0, hl);
+    st |= ilqr_traj<T, NA, LPT>(s, cn, cfn, xn0, Xn, Un, gains, none, 0, none, itn, pr, 0, hl,
+                                a.choices ? a.choices + i : nullptr, nb);
     // ancillary MPC tracking the nominal plan :863-909 (terminal weight Qa, :885, :891)
     DCost<T> ca;
     ca.kind = DTMPC_COST_TRACK;
@@ -302,7 +308,8 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
     ca.t0 = ca.t1 = ca.t2 = T(0);
     T xa0[4] = {x0, x1, x2, xb};
     pr.mark(8);
-    st |= ilqr_traj<T, NA, LPT>(s, ca, cfa, xa0, Xa, Ua, gains, Xn, 4, Un, ita, pr, 4, hl);
+    st |= ilqr_traj<T, NA, LPT>(s, ca, cfa, xa0, Xa, Ua, gains, Xn, 4, Un, ita, pr, 4, hl,
+                                a.choices ? a.choices + (size_t)cfn.max_iter * nb + i : nullptr, nb);
     pr.mark(8);
     // upper loss, DOC sensitivity and analytic gradient :915-976
     st |= sens_traj<T, false, false, true>(s, ca, Xa, Ua, Xn, 4, Un, Xn, 4, K, kf, AB, none, none,
@@ -369,7 +376,9 @@ tube_step_kernel(DSpec<T> s_arg, DCost<T> cn, DIlqr<T> cfn, DIlqr<T> cfa, TubeAr
     // batch sums over the healthy trajectories only (L and gradients, and their count in slot 7):
     // a flagged trajectory drops out of the mean; a pair counts once
     acc[7] = T(1);
-    if (st || hl != 0) {
+    bool within = true;  // every gradient component within the health bound (NaN fails)
+    for (int j = 1; j < 7; ++j) within = within && (m_abs(acc[j]) <= a.gbound);
+    if (st || hl != 0 || !within) {
 #pragma unroll
       for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) acc[j] = T(0);
     }
@@ -442,21 +451,22 @@ __global__ void theta_update_kernel(T mom, T eta, T qmin, T rmin, T qbmin, T qbm
 template <typename T, int NA>
 static void launch_ilqr_na(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, int B,
                            const void* x0, const void* Xref, const void* Uref, void* X, void* U,
-                           void* K, void* kff, int* iters, int* status, hipStream_t st) {
+                           void* K, void* kff, int* iters, int* status, signed char* choices, hipStream_t st) {
   hipLaunchKernelGGL((ilqr_kernel<T, NA>), grid_for(B), dim3(kBlock), 0, st, s, c, cfg, B, x0, Xref,
-                     Uref, X, U, K, kff, iters, status);
+                     Uref, X, U, K, kff, iters, status, choices);
 }
 
 template <typename T>
 static int launch_ilqr(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf,
                        int64_t B, const void* x0, const void* Xref, const void* Uref, void* X,
-                       void* U, void* K, void* kff, int* iters, int* status, hipStream_t st) {
+                       void* U, void* K, void* kff, int* iters, int* status, signed char* choices,
+                       hipStream_t st) {
   DSpec<T> s = make_spec<T>(*sp);
   DCost<T> c = make_cost<T>(*cp);
   DIlqr<T> cfg = make_ilqr<T>(*cf);
   switch (cfg.nc) {  // rolled-out candidates (alpha = 0 is taken from the previous iteration)
 #define CASE(n) \
-  case n: launch_ilqr_na<T, n>(s, c, cfg, (int)B, x0, Xref, Uref, X, U, K, kff, iters, status, st); break;
+  case n: launch_ilqr_na<T, n>(s, c, cfg, (int)B, x0, Xref, Uref, X, U, K, kff, iters, status, choices, st); break;
     DTMPC_NA_CASES(CASE)
 #undef CASE
     default: return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
@@ -491,6 +501,8 @@ static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B
   a.status = S->status;
   a.iters = S->iters;
   a.w = (const T*)w;
+  a.choices = (signed char*)S->choices;
+  a.gbound = cf->grad_bound > 0 ? T(cf->grad_bound) : T(__builtin_inf());
   a.disturbance = cf->disturbance;
   a.write_log = (cf->write_log && S->log) ? 1 : 0;
   a.seed = cf->seed;
@@ -624,15 +636,16 @@ int dtmpc_linearize(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, i
 int dtmpc_ilqr_solve(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
                      const dtmpc_ilqr_cfg* cfg, int64_t B, const void* x0, const void* Xref,
                      const void* Uref, void* X, void* U, void* K, void* kff, int32_t* iters,
-                     int32_t* status, void* stream) {
+                     int32_t* status, int8_t* choices, void* stream) {
   int e = check_spec(spec, B);
   if (e) return e;
   if ((e = check_cost(cost, Xref, Uref))) return e;
   if ((e = check_ilqr(cfg))) return e;
   if (!x0 || !X || !U || !K || !kff || !status) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == DTMPC_F32) return launch_ilqr<float>(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, st);
-  if (dtype == DTMPC_F64) return launch_ilqr<double>(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, st);
+  signed char* ch = (signed char*)choices;
+  if (dtype == DTMPC_F32) return launch_ilqr<float>(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, ch, st);
+  if (dtype == DTMPC_F64) return launch_ilqr<double>(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, ch, st);
   return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
 }
 

@@ -611,11 +611,15 @@ constexpr bool kPackedLS = DTMPC_LS_PACKED != 0;
 // ---------------------------------------------------------------------------------------------
 // iLQR for one trajectory (core/ddp.py:102-307).  U: in V_init, out V*.  X: out X*.
 // K/kf: scratch + gains of the last backward pass.  Returns DTMPC_ST_* bits.
+// ch (or NULL): the decision record -- the winning alpha's original position of iteration it at
+// ch[it * chs], -1 for iterations not run (written by lane h == 0).
 template <typename T, int NA, int LPT = 1, typename G = GainsSoA<T>>
 __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, const T* x0,
                          const Col<T>& X, const Col<T>& U, const G& gains,
                          const Col<T>& Xr, int rf, const Col<T>& Ur, int& iters, Prof& pr,
-                         int pb, int h = 0) {
+                         int pb, int h = 0, signed char* ch = nullptr, size_t chs = 0) {
+  if (ch && h == 0)
+    for (int it = 0; it < cfg.max_iter; ++it) ch[it * chs] = -1;
   // V = clamp(V_init); X = rollout(x0, V)   (:127-131); the cost of that tape is the alpha = 0
   // candidate's cost (only needed when alpha = 0 is listed)
   T Jcur = init_tape(s, c, x0, X, U, Xr, rf, Ur, cfg.zpos >= 0 && cfg.max_iter > 0);
@@ -646,6 +650,7 @@ __device__ __forceinline__ int ilqr_traj(const DSpec<T>& s, const DCost<T>& c, c
 #endif
     pr.mark(pb + 2);
     if (best < 0) return DTMPC_ST_NONFINITE;
+    if (ch && h == 0) ch[it * chs] = (signed char)best;
     if (al != T(0)) commit_candidate(s, al, x0, Bc0, X, U, gains);
 #ifdef DTMPC_DIAG_CM2  // timing attribution only: a second rollout (results change)
     __asm__ volatile("" ::: "memory");

@@ -94,6 +94,7 @@ class DtmpcTubeCfg(C.Structure):
         ("seed", C.c_uint64),
         ("w_low", C.c_double * 3),
         ("w_high", C.c_double * 3),
+        ("grad_bound", C.c_double),
     ]
 
 
@@ -118,6 +119,7 @@ class DtmpcTubeState(C.Structure):
         ("n_partials", C.c_int64),
         ("chunk", C.c_int64),
         ("work_bytes", C.c_int64),
+        ("choices", C.c_void_p),
     ]
 
 
@@ -184,7 +186,8 @@ PROTOTYPES = {
     ),
     "dtmpc_ilqr_solve": (
         C.c_int,
-        [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, P, P, P, P, P, P, P, P, P, P],
+        [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, P, P, P, P, P, P, P, P, P, P,
+         P],
     ),
     "dtmpc_sensitivity_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64, I32]),
     "dtmpc_ddp_sensitivity": (

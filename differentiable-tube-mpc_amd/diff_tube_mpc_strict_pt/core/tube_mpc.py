@@ -33,7 +33,10 @@ from .ddp import _dtype_code, raise_for_status
 from .problem import GeneralSetup, PaperSetup, general_setup_from_config, paper_setup_from_config, softplus
 
 __all__ = ["ExperimentTrajectories", "TubeMPC", "GeneralTubeMPC", "run_closed_loop_experiment", "shard_range",
-           "allreduce_sums"]
+           "allreduce_sums", "DEFAULT_GRAD_BOUND_F32"]
+
+# f32 health bound on a trajectory's DOC gradient components (TubeMPC grad_bound, dtmpc_tube_cfg.grad_bound)
+DEFAULT_GRAD_BOUND_F32 = 1e6
 
 
 @dataclass
@@ -89,11 +92,18 @@ class TubeMPC:
         (pass w to :meth:`step`).
       global_offset / global_batch: position of this shard in the global batch (multi-GPU).
       write_log: keep the per-step record (x, u, xbar, ubar, b, L, gQ, gR, gqb) on device.
+      record_choices: keep the step's decision record (``choices`` [I_nom + I_aux, B] int8: the winning
+        line-search alpha position of every nominal, then ancillary iteration, -1 not run).
+      grad_bound: health policy of the shared update -- a trajectory whose DOC gradient row has a
+        component above this magnitude drops out of the batch mean like a flagged one.  Default: 1e6 in
+        f32 (the reference's own f32 path overflows on such trajectories: obstacle-grazing ancillary plans
+        give |g| ~ 1e15-1e30 against ~1e2 typical), none in f64.  At B = 1 on the reference's closed loop
+        the bound never triggers, so the update is the reference's exactly (tests/test_gpu_parity.py).
     """
 
     def __init__(self, setup, *, batch: int, device="cuda", dtype=torch.float32, disturbance: str = "philox",
                  seed: int = 0, global_offset: int = 0, global_batch: Optional[int] = None, process_group=None,
-                 write_log: bool = False):
+                 write_log: bool = False, record_choices: bool = False, grad_bound: Optional[float] = None):
         if isinstance(setup, dict):
             setup = paper_setup_from_config(setup)
         self.setup: PaperSetup = setup
@@ -124,6 +134,9 @@ class TubeMPC:
         for f in range(3):
             cfg.w_low[f] = float(setup.w_low[f])
             cfg.w_high[f] = float(setup.w_high[f])
+        if grad_bound is None:
+            grad_bound = DEFAULT_GRAD_BOUND_F32 if dtype == torch.float32 else 0.0
+        cfg.grad_bound = float(grad_bound)
         self.cfg = cfg
         self.adapt = setup.adapt.to_c()
         kw = dict(dtype=dtype, device=self.device)
@@ -153,6 +166,9 @@ class TubeMPC:
         self.status = torch.zeros(B, dtype=torch.int32, device=self.device)
         self.iters = torch.zeros(2, B, dtype=torch.int32, device=self.device)
         self.log = torch.zeros(_abi.LOG_FIELDS, B, **kw) if write_log else None
+        nch = setup.ilqr_nom.max_iter + setup.ilqr_aux.max_iter
+        self.choices = (torch.full((max(nch, 1), B), -1, dtype=torch.int8, device=self.device)
+                        if record_choices else None)
         self.t = 0
         st = _abi.DtmpcTubeState()
         st.x, st.b, st.xbar, st.bbar = (t.data_ptr() for t in (self.x, self.b, self.xbar, self.bbar))
@@ -167,6 +183,7 @@ class TubeMPC:
         st.n_partials = self.n_partials
         st.chunk = self.chunk
         st.work_bytes = wbytes
+        st.choices = self.choices.data_ptr() if self.choices is not None else None
         self.state = st
 
     # -----------------------------------------------------------------------------------------

@@ -141,6 +141,10 @@ typedef struct dtmpc_tube_cfg {
   uint64_t seed;            /* Philox key (disturbance == 1) */
   double w_low[3];
   double w_high[3];
+  double grad_bound;        /* health policy of the shared update: a trajectory whose DOC gradient row
+                               [gQ, gR, gqb] has a component of magnitude above grad_bound (or a
+                               non-finite one) drops out of the batch sums like a flagged trajectory;
+                               <= 0 disables the bound (only status flags exclude) */
 } dtmpc_tube_cfg;
 
 /* Device-resident closed-loop state; all SoA [fields][B] unless stated, caller-owned. */
@@ -156,7 +160,8 @@ typedef struct dtmpc_tube_state {
   void* work;       /* dtmpc_tube_workspace_bytes() scratch */
   const void* theta;/* [6] ancillary weights Qa(3), Ra(2), qba (shared by the batch) */
   void* partials;   /* [n_partials][8] per-workgroup sums over the HEALTHY trajectories (status 0
-                       after this step): L, gQ(3), gR(2), gqb, and their count */
+                       after this step and a gradient row within cfg->grad_bound): L, gQ(3), gR(2),
+                       gqb, and their count */
   void* log;        /* [18][B] or NULL: x(3) u(2) xbar(3) ubar(2) b L gQ(3) gR(2) gqb of step t
                        (the gradient rows are the trajectory's own contribution before any
                        status masking) */
@@ -169,6 +174,10 @@ typedef struct dtmpc_tube_state {
                        dtmpc_tube_chunk(horizon, lanes) */
   int64_t work_bytes; /* size of `work`; must be >=
                          dtmpc_tube_workspace_bytes(dtype, horizon, B, lanes, chunk) */
+  int8_t* choices;  /* [nom_ilqr.max_iter + aux_ilqr.max_iter][B] or NULL: the decision record of the
+                       step -- per iteration of the nominal, then the ancillary solve, the
+                       original position of the winning line-search alpha (core/ddp.py:293, strict <,
+                       first wins), -1 for iterations not run */
 } dtmpc_tube_state;
 
 int dtmpc_abi_version(void);
@@ -206,12 +215,15 @@ int dtmpc_linearize(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, i
 /* Box-clamped iLQR with line search (all alphas, best-of, strict <) and per-trajectory tol exit:
  *   replaces core/ddp.py:102-307 `ilqr_solve` for the typed problem.
  *   x0 [4][B]; U [N][2][B] in: V_init (clamped first, core/ddp.py:127-129), out: V*;
- *   X [N+1][4][B] out: X*; K [N][8][B] / kff [N][2][B] out: gains of the last backward pass
- *   (may be NULL); iters [B] out (may be NULL); status [B] out (OR-accumulated). */
+ *   X [N+1][4][B] out: X*; K [N][8][B] / kff [N][2][B] out: gains of the last backward pass (scratch
+ *   of the solve, required); iters [B] out (may be NULL); status [B] out (OR-accumulated);
+ *   choices [cfg->max_iter][B] out or NULL: the winning line-search alpha's original position per
+ *   iteration (core/ddp.py:293), -1 for iterations not run. */
 int dtmpc_ilqr_solve(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
                      const dtmpc_ilqr_cfg* cfg, int64_t B, const void* x0,
                      const void* Xref, const void* Uref, void* X, void* U,
-                     void* K, void* kff, int32_t* iters, int32_t* status, void* stream);
+                     void* K, void* kff, int32_t* iters, int32_t* status, int8_t* choices,
+                     void* stream);
 
 /* Scratch bytes for dtmpc_ddp_sensitivity. */
 size_t dtmpc_sensitivity_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t want_lambda);
@@ -245,7 +257,7 @@ int64_t dtmpc_tube_chunk(int32_t horizon, int32_t lanes);
  * 0 if lanes is not a supported count or chunk is not one dtmpc_tube_chunk can return. */
 size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t lanes, int64_t chunk);
 /* Lanes per trajectory the fused step uses for a batch of B on the current device (lane slots =
- * CUs x 4 SIMDs x 64, 65,536 on MI355X): 4 while 4 B <= slots (B <= 16,384: one line-search pair per
+ * CUs x 4 SIMDs x 64, 65,536 on MI355X): 4 while 8 B <= slots (B <= 8,192: one line-search pair per
  * lane, candidate tapes kept instead of a commit pass), 2 while 2 B <= slots (paired line search),
  * else 1 (one wave per SIMD at the benchmark batch); the environment variable DTMPC_TUBE_LANES=1|2|4
  * overrides.  Resolved ONCE, when the caller builds its state (dtmpc_tube_state.lanes);

@@ -77,3 +77,48 @@ def tol_for(dtype, cond: float) -> float:
     """Comparison tolerance from the reference's own conditioning on that case."""
     base = 1e-9 if np.dtype(dtype) == np.float64 else 2e-3
     return max(base, 100.0 * float(cond))
+
+
+def active_set(U, u_min=(-10.0, -np.pi), u_max=(10.0, np.pi), tol: float = 1e-8):
+    """BoxClampControl.active_mask (core/control.py:66-70) of plans U [..., 2]."""
+    U = np.asarray(U, np.float64)
+    lo, hi = np.asarray(u_min, np.float64), np.asarray(u_max, np.float64)
+    return (U <= lo + tol) | (U >= hi - tol)
+
+
+def decision_agreement(dev_ch, oracle_chs, dev_U=None, oracle_Us=None, label: str = "", show: int = 6):
+    """Decision record agreement.  dev_ch / oracle_chs: per trajectory the sequence of
+    winning line-search alpha positions ([B, I] int, -1 = iteration not run) of the device and of each
+    oracle build; dev_U / oracle_Us: final plans [B, N, 2] whose active sets (core/control.py:66-70) are
+    compared too.  Near-ties of the line-search costs make the decision rounding-dependent, so the
+    oracle builds (same algorithm, three roundings) disagree among themselves on part of the batch; the
+    gate is therefore taken on the DETERMINATE trajectories -- those on which all builds agree -- where
+    the device must make the same decisions, and the overall rate (device = at least one build) is
+    reported beside the builds' own mutual agreement.  Prints a summary and the first disagreements."""
+    dev_ch = np.asarray(dev_ch)
+    chs = [np.asarray(c) for c in oracle_chs]
+    B = dev_ch.shape[0]
+    eq = np.stack([(dev_ch == c).all(1) for c in chs])  # [builds, B]
+    det = np.stack([(c == chs[0]).all(1) for c in chs[1:]]).all(0)
+    ok_any = eq.any(0)
+    if dev_U is not None:
+        da = active_set(dev_U).reshape(B, -1)
+        acts = [active_set(u).reshape(B, -1) for u in oracle_Us]
+        aeq = np.stack([(da == a).all(1) for a in acts])
+        det = det & np.stack([(a == acts[0]).all(1) for a in acts[1:]]).all(0)
+        ok_any = ok_any & (eq & aeq).any(0)
+        eq0 = eq[0] & aeq[0]
+    else:
+        eq0 = eq[0]
+    n_det = int(det.sum())
+    res = {"n": int(B), "determinate": n_det / B, "on_determinate": float(eq0[det].mean()) if n_det else 1.0,
+           "overall": float(ok_any.mean()), "oracle_builds_agree": n_det / B}
+    bad = np.nonzero(det & ~eq0)[0]
+    res["disagree_determinate"] = bad.tolist()
+    print(f"[decisions{(' ' + label) if label else ''}] B={B}: alpha sequence"
+          + (" + active set" if dev_U is not None else "")
+          + f" -- on the {n_det} determinate trajectories (all oracle builds agree) {res['on_determinate']:.4f}; "
+          f"overall (device = one of the builds) {res['overall']:.4f}; {len(bad)} determinate disagreements")
+    for i in bad[:show]:
+        print(f"    traj {i}: device {dev_ch[i].tolist()} oracle {chs[0][i].tolist()}")
+    return res

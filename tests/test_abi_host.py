@@ -99,7 +99,7 @@ def test_arguments_validated_before_any_device_call(lib):
     cfg = st.ilqr_nom.to_c()
     cfg.n_alphas = 0
     rc = lib.dtmpc_ilqr_solve(_abi.F32, C.byref(spec), C.byref(cost), C.byref(cfg), 4, 1, None, None, 1, 1, 1, 1, None,
-                              1, None)
+                              1, None, None)
     assert rc == _abi.ERR_BAD_ARG and b"n_alphas" in lib.dtmpc_last_error()
     bad = st.problem.to_c()
     bad.dbas_gamma = 1.5

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from _common import CHAOTIC, agreement, golden, ilqr_cfg, oracles, paper_setup, rel, tol_for
+from _common import decision_agreement, CHAOTIC, agreement, golden, ilqr_cfg, oracles, paper_setup, rel, tol_for
 
 pytestmark = pytest.mark.gpu
 
@@ -150,6 +150,18 @@ def test_ilqr_ancillary_sensitivity_grad_vs_reference_golden(dev, oracle_lib, ta
 
 
 # ------------------------------------------------------------------------------------ solvers vs oracle, batched
+# decision-record gate (the chosen alpha of every iteration + the final active set) on the
+# determinate trajectories, those on which the three oracle builds agree (tests/_common.py
+# decision_agreement; near-ties of line-search costs at the working precision make the rest
+# rounding-dependent in the oracle itself)
+# Measured (round 3, profiles/r03/decisions.txt): f64 >= 0.99 everywhere.  In f32 the device's own rounding
+# (hardware exp / log / rcp, fused multiply-adds) is none of the three builds', and the f32 line-search
+# costs tie at fp32 resolution near convergence, so even where the builds agree the device's decision
+# differs on a few percent of iLQR solves and on ~10 % of the 30-iteration tube steps (late iterations,
+# alpha = 0.01 vs keep); the f32 gates are set below those measurements, the rates are printed.
+DECISION_GATE = {"f64": 0.99, "f32": 0.95}
+DECISION_GATE_TUBE = {"f64": 0.99, "f32": 0.84}
+
 @pytest.mark.parametrize("tag", ["f64", "f32"])
 def test_ilqr_batched_vs_oracle(dev, oracle_lib, tag):
     """Ragged batch (B = 1000) of random starts / warm starts; nominal cost with fixed iterations and
@@ -166,25 +178,32 @@ def test_ilqr_batched_vs_oracle(dev, oracle_lib, tag):
     x0, V0 = random_batch(B, 5, npdt)
     for cost, mi, tl in ((st.nominal_cost, 5, -1.0), (st.nominal_cost, 10, 1e-3)):
         r = ilqr_solve(problem=st.problem, cost=cost, cfg=ilqr_cfg(mi, tl), x0=_t(x0, tdt, dev), V_init=_t(V0, tdt, dev),
-                       check=False)
-        outs = [o.ilqr_solve(sp, cost.to_c(), ilqr_cfg(mi, tl).to_c(), x0, V0) for o in ors]
+                       check=False, record_choices=True)
+        outs = [o.ilqr_solve(sp, cost.to_c(), ilqr_cfg(mi, tl).to_c(), x0, V0, choices=True) for o in ors]
         Xp, Vp, so = outs[0][0], outs[0][1], outs[0][5]
         keep = (so == 0) & (r.status.cpu().numpy() == 0)
         assert keep.mean() > 0.995
         frac, e, s = agreement(r.X.cpu().numpy()[keep], [o[0][keep] for o in outs], base)
         assert frac >= 0.99, (mi, tl, frac, np.sort(e)[-5:])
+        # decision record: winning alpha per iteration + final active set
+        dec = decision_agreement(r.choices.cpu().numpy()[keep], [o[6][keep] for o in outs], r.V.cpu().numpy()[keep],
+                                 [o[1][keep] for o in outs], label=f"ilqr {tag} max_iter={mi} tol={tl}")
+        assert dec["on_determinate"] >= DECISION_GATE[tag], dec
     cost = tracking_cost((0.7, 1.3, 0.2, 0.5, 2.0, 0.8))
     xa = x0.copy()
     xa[:, :2] += 0.02
     Va0 = np.roll(Vp, -1, axis=1)
     r = ilqr_solve(problem=st.problem, cost=cost, cfg=ilqr_cfg(20, 1e-3), x0=_t(xa, tdt, dev), V_init=_t(Va0, tdt, dev),
-                   X_ref=_t(Xp, tdt, dev), U_ref=_t(Vp, tdt, dev), check=False)
+                   X_ref=_t(Xp, tdt, dev), U_ref=_t(Vp, tdt, dev), check=False, record_choices=True)
     args = (sp, cost.to_c(), ilqr_cfg(20, 1e-3).to_c(), xa, Va0, Xp, Vp)
-    outs = [o.ilqr_solve(*args) for o in ors]
+    outs = [o.ilqr_solve(*args, choices=True) for o in ors]
     keep = (outs[0][5] == 0) & (r.status.cpu().numpy() == 0)
     assert keep.mean() > 0.99
     frac, e, s = agreement(r.X.cpu().numpy()[keep], [o[0][keep] for o in outs], base)
     assert frac >= 0.98, (frac, np.sort(e)[-5:])
+    dec = decision_agreement(r.choices.cpu().numpy()[keep], [o[6][keep] for o in outs], r.V.cpu().numpy()[keep],
+                             [o[1][keep] for o in outs], label=f"ilqr {tag} tracking")
+    assert dec["on_determinate"] >= DECISION_GATE[tag], dec
 
 
 @pytest.mark.parametrize("tag", ["f64", "f32"])
@@ -367,7 +386,8 @@ def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode, lanes, monkeypatch):
     B = 700
     rng = np.random.default_rng(11)
     x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(npdt)
-    mpc = TubeMPC(st, batch=B, device=dev, dtype=tdt, disturbance="philox", seed=3, write_log=True)
+    mpc = TubeMPC(st, batch=B, device=dev, dtype=tdt, disturbance="philox", seed=3, write_log=True,
+                  record_choices=True)
     mpc.reset(_t(x, tdt, dev))
     ors = oracles(npdt)
     base = 1e-9 if tag == "f64" else 1e-4
@@ -382,13 +402,22 @@ def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode, lanes, monkeypatch):
         outs = []
         for o in ors:
             state = {k: v.copy() for k, v in pre.items()}
-            gout, _, so, _ = o.tube_step(st.problem.to_c(), _tube_cfg(st, 3), state, th0, step=t)
+            gout, _, so, _, ch = o.tube_step(st.problem.to_c(), _tube_cfg(st, 3), state, th0, step=t, choices=True)
             sums = np.zeros(8, npdt)
             sums[:7] = gout.sum(1)
             theta, _ = o.theta_update(st.adapt.to_c(), 1.0 / B, sums, th0, vel0)
-            outs.append((state, theta, so, gout))
+            outs.append((state, theta, so, gout, ch))
         keep = (mpc.status.cpu().numpy() == 0) & (outs[0][2] == 0)
         assert keep.mean() > 0.99
+        # decision record: the nominal then ancillary winning alphas of every iteration and
+        # the final ancillary active set, against the oracle builds from the same pre-step state
+        # (active sets of the ancillary plans as the step leaves them: shifted warm starts on both sides)
+        dch = mpc.choices.cpu().numpy().T[keep]
+        dU = np.transpose(mpc.Uaux.cpu().numpy(), (2, 0, 1))[keep]
+        dec = decision_agreement(dch, [o_[4].T[keep] for o_ in outs], dU,
+                                 [np.transpose(o_[0]["Uaux"], (2, 0, 1))[keep] for o_ in outs],
+                                 label=f"tube {tag} {mode} lanes={lanes} step {t}")
+        assert dec["on_determinate"] >= DECISION_GATE_TUBE[tag], dec
         for k in ("x", "xbar", "b"):
             dev_k = getattr(mpc, k).cpu().numpy()
             dev_k = dev_k.T if dev_k.ndim == 2 else dev_k[:, None]
@@ -408,6 +437,9 @@ def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode, lanes, monkeypatch):
         # obstacle-grazing trajectories whose gradients are chaotic -- the three CPU builds' thetas
         # already differ by up to 3e4 relative on this batch.)
         healthy = mpc.status.cpu().numpy() == 0
+        gb = mpc.cfg.grad_bound  # the health policy's bound on the gradient components (f32 default)
+        if gb > 0:
+            healthy &= (np.abs(log[12:18]) <= gb).all(0)
         g = np.where(healthy, log[11:18], 0).astype(np.float64)
         sums = np.zeros(8)
         sums[:7] = g.sum(1)
@@ -483,6 +515,63 @@ def test_closed_loop_vs_reference_loop_f64(dev):
     assert rel(th[:, 0:3], g["Qa_history"]) < t
     assert rel(th[:, 3:5], g["Ra_history"]) < t
     assert rel(th[:, 5], g["qba_history"]) < t
+
+
+def test_closed_loop_vs_reference_loop_f32_health_policy(dev):
+    """TubeMPC(B=1) in f32 with the default health policy (grad_bound 1e6) reproduces the reference's own
+    f32 paper-mode loop: the bound never triggers there, so every theta update is the reference's
+    (core/tube_mpc.py:978-984) exactly as computed from the trajectory's gradient."""
+    from diff_tube_mpc_strict_pt.core import TubeMPC
+
+    g = golden("closed_loop_f32")
+    st = paper_setup()
+    mpc = TubeMPC(st, batch=1, device=dev, dtype=torch.float32, disturbance="injected", write_log=True)
+    assert mpc.cfg.grad_bound == 1e6
+    mpc.reset(torch.tensor([[0.0, 0.0, np.pi / 4]], dtype=torch.float32))
+    logs, th = [], []
+    for t in range(g["loss"].shape[0]):
+        mpc.step(_t(g["w"][t:t + 1], torch.float32, dev))
+        assert mpc.healthy_count == 1
+        logs.append(mpc.log[:, 0].cpu().numpy())
+        th.append(mpc.theta.cpu().numpy())
+    logs, th = np.array(logs), np.array(th)
+    t = 5e-4  # the oracle's f32 tolerance against the same fixture (tests/test_oracle_golden.py)
+    assert rel(logs[:, 0:3], g["x_real"]) < t
+    assert rel(logs[:, 11], g["loss"]) < t
+    assert rel(th[:, 0:3], g["Qa_history"]) < t
+    assert rel(th[:, 3:5], g["Ra_history"]) < t
+    assert rel(th[:, 5], g["qba_history"]) < t
+
+
+def test_free_running_loop_f32_theta_bounded(dev):
+    """The steady-state workload of bench.py: B = 65,536 f32, fixed iterations, 20 free-running closed-loop
+    steps (warm-started, theta updated every step under the f32 health policy) keep theta finite and
+    bounded and nearly every trajectory healthy (measured: ~98.5 % per step; the rest are flagged or
+    obstacle-grazing outliers the health policy drops)."""
+    import dataclasses
+
+    from diff_tube_mpc_strict_pt.core import TubeMPC
+
+    st = paper_setup()
+    st = dataclasses.replace(st, ilqr_nom=dataclasses.replace(st.ilqr_nom, tol=-1.0),
+                             ilqr_aux=dataclasses.replace(st.ilqr_aux, tol=-1.0))
+    B = 65536
+    g = torch.Generator().manual_seed(0)
+    u = torch.rand(B, 3, generator=g, dtype=torch.float64)
+    x0 = torch.stack([u[:, 0], u[:, 1], u[:, 2] * (np.pi / 2)], 1).float()
+    m = TubeMPC(st, batch=B, device=dev, dtype=torch.float32, disturbance="philox", seed=0)
+    m.reset(x0)
+    thetas, healthy = [], []
+    for _ in range(20):
+        m.step()
+        thetas.append(m.theta.double().cpu().numpy())
+        healthy.append(m.healthy_count / B)
+    thetas = np.array(thetas)
+    print(f"[free-running f32 B={B}] theta after 20 steps {thetas[-1].round(4).tolist()}, "
+          f"max |theta| {np.abs(thetas).max():.4g}, healthy fraction min {min(healthy):.5f}")
+    assert np.isfinite(thetas).all()
+    assert np.abs(thetas).max() < 1e3, thetas.max(0)
+    assert min(healthy) > 0.97, healthy
 
 
 def test_run_closed_loop_experiment_outputs(dev, tmp_path):
