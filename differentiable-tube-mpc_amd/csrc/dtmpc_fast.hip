@@ -1995,6 +1995,25 @@ tube_fast_kernel(FK kk) {
   }
 }
 
+// Known-byte calibration launch for the HBM counters (scripts/pmc_calib.py, rocprofv3 --pmc FETCH_SIZE /
+// WRITE_SIZE): the fast kernel's own access pattern -- per-lane 16-byte X records and 8-byte U records
+// [rows][B][W] through one buffer resource, loaded and stored row by row -- copied from src to dst, so
+// the counters' ratio to the known bytes corrects the tube step's figures (MI355X_MICROARCH.md §HBM:
+// "calibrate on a known byte count in your own access pattern").
+__global__ void __launch_bounds__(kBlock) record_stream_kernel(const float* src, float* dst, int B, int N,
+                                                               unsigned bytes) {
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= B) return;
+  const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)bytes, 0x00020000);
+  const Rsrc rd = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)bytes, 0x00020000);
+  const unsigned cb = (unsigned)B, X = cb * (N + 1) * 16u;
+  const RA XA{0, cb * 16u, (unsigned)t * 16u}, UA{X, cb * 8u, (unsigned)t * 8u};
+  for (int k = 0; k <= N; ++k) {
+    rst4(rd, XA, k, 0, rld4(rs, XA, k, 0));
+    if (k < N) rst2(rd, UA, k, 0, rld2(rs, UA, k, 0));
+  }
+}
+
 }  // namespace fk
 
 // ---------------------------------------------------------------------------------------------
@@ -2194,6 +2213,18 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
 }
 
 }  // namespace dtmpc
+
+extern "C" {
+// diagnostics (not part of include/dtmpc.h): the counter-calibration copy of record_stream_kernel over
+// src / dst buffers of (N+1) x 16 + N x 8 bytes per trajectory (< 2^31 bytes)
+int dtmpc_diag_record_stream(int64_t B, int32_t N, const void* src, void* dst, void* stream) {
+  const int64_t bytes = B * ((int64_t)(N + 1) * 16 + (int64_t)N * 8);
+  if (B < 1 || N < 1 || bytes >= 0x7fffffff || !src || !dst) return dtmpc::set_err(DTMPC_ERR_BAD_ARG, "bad sizes");
+  hipLaunchKernelGGL(dtmpc::fk::record_stream_kernel, dtmpc::grid_for(B), dim3(dtmpc::kBlock), 0, (hipStream_t)stream,
+                     (const float*)src, (float*)dst, (int)B, (int)N, (unsigned)bytes);
+  return dtmpc::check_launch("record_stream_kernel");
+}
+}
 
 #ifdef DTMPC_PROFILE
 extern "C" {

@@ -5,9 +5,12 @@ usage: python scripts/pmc_summary.py gpurun_out/prof_TAG OUT.json [--batch B]
 Per-dispatch means of every counter for the tube-step kernel (tube_fast_kernel, the specialised paper
 configuration, or the generic tube_step_kernel -- whichever the bench launched), plus the HBM bytes per launch:
   raw = FETCH_SIZE + WRITE_SIZE (KiB -> bytes), and the calibrated figure, where FETCH / WRITE are each
-  divided by the ratio measured/known on the known-byte rollout launch of scripts/pmc_calib.py (same
-  dword-per-lane access pattern, past the Infinity Cache).  MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE
-  reads 1/2 of wide 16-B/lane streams; other widths must be calibrated -- this does it for ours."""
+  divided by the ratio measured/known on the known-byte launch of scripts/pmc_calib.py (the tube kernel's
+  16-byte / 8-byte per-lane record pattern through one buffer resource, past the Infinity Cache).
+  MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE reads 1/2 of wide 16-B/lane streams; other widths must be
+  calibrated -- this does it for ours.
+The summary records the sha256 of the library the passes ran (bench.py refuses a summary of another
+build for its roofline `traffic` field)."""
 import csv
 import glob
 import json
@@ -50,14 +53,20 @@ def main():
     root, out = sys.argv[1], sys.argv[2]
     batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 65536
     tube = {k: v for sub in ("fetch", "write", "sq1", "sq2", "tcc") for k, v in counters(root, TUBE_KERNELS, sub).items()}
-    cal_f = counters(root, "rollout_kernel", "cal_fetch")
-    cal_w = counters(root, "rollout_kernel", "cal_write")
+    cal_f = counters(root, "record_stream_kernel", "cal_fetch")
+    cal_w = counters(root, "record_stream_kernel", "cal_write")
     N = 50
     Bc = 262144
-    known_r, known_w = 4 * Bc * (4 + 2 * N), 4 * Bc * 4 * (N + 1)
+    known_r = known_w = Bc * ((N + 1) * 16 + N * 8)
     ks = kernel_stats(root, TUBE_KERNELS)
+    import hashlib
+
+    lib = os.environ.get("DTMPC_LIBRARY") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                          "differentiable-tube-mpc_amd", "diff_tube_mpc_strict_pt",
+                                                          "libdtmpc.so")
     res = {"kernel": (ks or {}).get("name", "tube step") + " (7 alphas: 6 rolled out + alpha = 0 from the current tape)",
-           "batch": batch, "counters_per_dispatch": tube, "kernel_trace": ks}
+           "workload": "tube", "batch": batch, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+           "counters_per_dispatch": tube, "kernel_trace": ks}
     if "FETCH_SIZE" in tube and "WRITE_SIZE" in tube:
         raw = 1024.0 * (tube["FETCH_SIZE"] + tube["WRITE_SIZE"])
         res["tube_step_bytes_raw"] = raw
@@ -65,7 +74,7 @@ def main():
         if cal_f.get("FETCH_SIZE") and cal_w.get("WRITE_SIZE"):
             rf = 1024.0 * cal_f["FETCH_SIZE"] / known_r
             rw = 1024.0 * cal_w["WRITE_SIZE"] / known_w
-            res["calibration"] = {"kernel": "rollout_kernel<float>", "batch": Bc, "known_read_bytes": known_r,
+            res["calibration"] = {"kernel": "record_stream_kernel", "batch": Bc, "known_read_bytes": known_r,
                                   "known_write_bytes": known_w, "fetch_measured_over_known": rf,
                                   "write_measured_over_known": rw}
             res["tube_step_bytes_per_launch"] = 1024.0 * (tube["FETCH_SIZE"] / rf + tube["WRITE_SIZE"] / rw)
