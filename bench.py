@@ -148,6 +148,85 @@ def cpu_baseline(setup, seconds_target: float = 15.0):
                       f"(10+20 fixed iLQR iterations, 7 alphas, + IFT), OpenMP {threads} threads, {dt:.1f} s"}
 
 
+def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup: int = 3):
+    """BASELINE config 2: batched nominal DDP (Dubins n = 3, m = 2 + barrier state, T = 50) over B
+    trajectories on one GPU -- dtmpc_ilqr_solve with the nominal target cost, 10 fixed iterations
+    (tol = -1), 7 line-search alphas, zero warm start.  One step = one solve of the whole batch from the
+    same x0 / V_init (the control tape is re-seeded inside the timed region: it is the in/out buffer)."""
+    import ctypes as C
+    import dataclasses
+
+    from diff_tube_mpc_strict_pt import _lib
+    from diff_tube_mpc_strict_pt.core.ddp import _prep_x0, dbas_init
+
+    dt = torch.float32 if dtype_name == "f32" else torch.float64
+    st = bench_setup(dtype_name)
+    cfg = dataclasses.replace(st.ilqr_nom, tol=-1.0)
+    N = st.problem.horizon
+    lib = _lib.load()
+    spec, cc, ic = st.problem.to_c(), st.nominal_cost.to_c(), cfg.to_c()
+    x3 = initial_states(0, B, dev, dt)
+    x0 = _prep_x0(torch.cat([x3, dbas_init(st.problem, x3)[:, None]], 1))  # b0 = B(h(x0))
+    kw = dict(dtype=dt, device=dev)
+    U0 = torch.zeros(N, 2, B, **kw)
+    Us, Xs = torch.empty_like(U0), torch.empty(N + 1, 4, B, **kw)
+    Ks, ks = torch.empty(N, 8, B, **kw), torch.empty(N, 2, B, **kw)
+    iters = torch.zeros(B, dtype=torch.int32, device=dev)
+    status = torch.zeros(B, dtype=torch.int32, device=dev)
+    code = 0 if dt == torch.float32 else 1
+
+    def solve():
+        Us.copy_(U0)
+        _lib.check(lib.dtmpc_ilqr_solve(code, C.byref(spec), C.byref(cc), C.byref(ic), B, x0.data_ptr(), None, None,
+                                        Xs.data_ptr(), Us.data_ptr(), Ks.data_ptr(), ks.data_ptr(), iters.data_ptr(),
+                                        status.data_ptr(), None, _lib.stream_of(x0)), "dtmpc_ilqr_solve")
+
+    for _ in range(warmup):
+        solve()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in ev:
+        e0.record()
+        solve()
+        e1.record()
+    torch.cuda.synchronize(dev)
+    wall = (time.perf_counter() - t0) / steps
+    return {"workload": f"BASELINE config 2: batched nominal DDP, {cfg.max_iter} fixed iterations (tol=-1), "
+                        f"{len(cfg.line_search_alphas)} alphas, T={N}, zero warm start",
+            "batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall,
+            "event_ms_median": float(np.median([a.elapsed_time(b) for a, b in ev])),
+            "value": B * cfg.max_iter / wall, "unit": "DDP iters/s",
+            "nonzero_status": int((status != 0).sum())}
+
+
+def tube_leg(dev, dtype_name: str, B: int, steps: int, warmup: int):
+    """The headline tube step (episode start) at another precision, one GPU, B trajectories."""
+    dt = torch.float32 if dtype_name == "f32" else torch.float64
+    setup = bench_setup(dtype_name)
+    mpc = TubeMPC(setup, batch=B, device=dev, dtype=dt, disturbance="philox", seed=0, global_offset=0,
+                  global_batch=B, process_group=None)
+    x0 = initial_states(0, B, dev, dt)
+    for _ in range(warmup):
+        mpc.reset(x0)
+        mpc.step()
+    torch.cuda.synchronize(dev)
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in kev:
+        mpc.reset(x0)
+        mpc.step(kernel_events=k)
+    torch.cuda.synchronize(dev)
+    wall = (time.perf_counter() - t0) / steps
+    out = {"batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall,
+           "kernel_ms": float(np.mean([a.elapsed_time(b) for a, b in kev])),
+           "value": B * ITERS_PER_STEP / wall, "unit": "DDP+IFT iters/s",
+           "flagged_trajectories": int((mpc.status != 0).sum()), "lanes": mpc.lanes}
+    del mpc
+    torch.cuda.empty_cache()
+    return out
+
+
 def _free_port() -> int:
     import socket
 
@@ -182,6 +261,10 @@ def main() -> None:
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo rehearsal of launch, sharding and timing with a placeholder step (no GPU)")
     ap.add_argument("--no-steady", action="store_true", help="skip the free-running (warm-started) loop field")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the secondary legs (f64 tube step, config-2 nominal DDP at B = 4096)")
+    ap.add_argument("--workload", default="tube", choices=["tube", "nominal-ddp"],
+                    help="nominal-ddp: print only the BASELINE config-2 line (one GPU)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -203,6 +286,17 @@ def main() -> None:
     world = dist.get_world_size() if dist.is_initialized() else 1
     if dist.is_initialized():
         rank = dist.get_rank()
+    if args.workload == "nominal-ddp":
+        if world != 1 or args.dry_run:
+            raise SystemExit("--workload nominal-ddp is a one-GPU leg")
+        leg = nominal_ddp_leg(dev, args.dtype, B=args.batch if args.batch != 65536 else 4096, steps=args.steps,
+                              warmup=args.warmup)
+        print(json.dumps({"metric": "batched nominal DDP iters/sec, Dubins+DBaS T=50", "value": leg["value"],
+                          "unit": leg["unit"], "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": leg["ms_per_step"], "higher_is_better": True, "scaling": "strong",
+                          "vs_baseline": None, "dtype": args.dtype, "data": "synthetic x0 (bench.initial_states)",
+                          "config": {"workload": leg["workload"], "global_batch": leg["batch"]}, "leg": leg}))
+        return
     dtype = torch.float32 if args.dtype == "f32" else torch.float64
     setup = bench_setup(args.dtype)
     Bg = args.batch * world if args.weak else args.batch
@@ -329,6 +423,15 @@ def main() -> None:
         },
     }
     out["steady_state"] = steady
+    if world == 1 and not args.dry_run and not args.no_extra:
+        # secondary legs: the reference's configured precision (configs/dubins.yaml:8,
+        # f64) on the same tube step, and BASELINE config 2 (batched nominal DDP, B = 4,096) in f32 / f64
+        other = "f64" if args.dtype == "f32" else "f32"
+        del mpc
+        torch.cuda.empty_cache()
+        out[f"tube_{other}"] = tube_leg(dev, other, Bg, steps=min(args.steps, 5), warmup=1)
+        out["nominal_ddp"] = {d: nominal_ddp_leg(dev, d, B=4096, steps=args.steps, warmup=args.warmup)
+                              for d in ("f32", "f64")}
     if args.dry_run:
         out["dry_run"] = True
     if rank == 0 and not args.no_cpu and world == 1 and not args.dry_run:
