@@ -148,11 +148,13 @@ def cpu_baseline(setup, seconds_target: float = 15.0):
                       f"(10+20 fixed iLQR iterations, 7 alphas, + IFT), OpenMP {threads} threads, {dt:.1f} s"}
 
 
-def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup: int = 3):
+def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup: int = 3, generic: bool = False):
     """BASELINE config 2: batched nominal DDP (Dubins n = 3, m = 2 + barrier state, T = 50) over B
-    trajectories on one GPU -- dtmpc_ilqr_solve with the nominal target cost, 10 fixed iterations
-    (tol = -1), 7 line-search alphas, zero warm start.  One step = one solve of the whole batch from the
-    same x0 / V_init (the control tape is re-seeded inside the timed region: it is the in/out buffer)."""
+    trajectories on one GPU -- dtmpc_ilqr_solve_ws (core.ddp.ilqr_solve's entry: the fused solver at the
+    default lane count; f64 runs the generic kernel) with the nominal target cost, 10 fixed iterations
+    (tol = -1), 7 line-search alphas, zero warm start; generic=True times dtmpc_ilqr_solve (the generic
+    kernel) instead.  One step = one solve of the whole batch from the same x0 / V_init (the control tape
+    is re-seeded inside the timed region: it is the in/out buffer)."""
     import ctypes as C
     import dataclasses
 
@@ -174,12 +176,22 @@ def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup
     iters = torch.zeros(B, dtype=torch.int32, device=dev)
     status = torch.zeros(B, dtype=torch.int32, device=dev)
     code = 0 if dt == torch.float32 else 1
+    lanes = int(lib.dtmpc_tube_lanes(B))
+    wb = int(lib.dtmpc_ilqr_workspace_bytes(code, N, B, lanes))
+    work = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
 
     def solve():
         Us.copy_(U0)
-        _lib.check(lib.dtmpc_ilqr_solve(code, C.byref(spec), C.byref(cc), C.byref(ic), B, x0.data_ptr(), None, None,
-                                        Xs.data_ptr(), Us.data_ptr(), Ks.data_ptr(), ks.data_ptr(), iters.data_ptr(),
-                                        status.data_ptr(), None, _lib.stream_of(x0)), "dtmpc_ilqr_solve")
+        if generic:
+            _lib.check(lib.dtmpc_ilqr_solve(code, C.byref(spec), C.byref(cc), C.byref(ic), B, x0.data_ptr(), None,
+                                            None, Xs.data_ptr(), Us.data_ptr(), Ks.data_ptr(), ks.data_ptr(),
+                                            iters.data_ptr(), status.data_ptr(), None, _lib.stream_of(x0)),
+                       "dtmpc_ilqr_solve")
+        else:
+            _lib.check(lib.dtmpc_ilqr_solve_ws(code, C.byref(spec), C.byref(cc), C.byref(ic), B, x0.data_ptr(), None,
+                                               None, Xs.data_ptr(), Us.data_ptr(), Ks.data_ptr(), ks.data_ptr(),
+                                               iters.data_ptr(), status.data_ptr(), None, lanes, work.data_ptr(), wb,
+                                               _lib.stream_of(x0)), "dtmpc_ilqr_solve_ws")
 
     for _ in range(warmup):
         solve()
@@ -195,6 +207,7 @@ def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup
     return {"workload": f"BASELINE config 2: batched nominal DDP, {cfg.max_iter} fixed iterations (tol=-1), "
                         f"{len(cfg.line_search_alphas)} alphas, T={N}, zero warm start",
             "batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall,
+            "kernel": ("generic ilqr_kernel" if generic or wb == 0 else f"fused ilqr_fast_kernel, {lanes} lanes"),
             "event_ms_median": float(np.median([a.elapsed_time(b) for a, b in ev])),
             "value": B * cfg.max_iter / wall, "unit": "DDP iters/s",
             "nonzero_status": int((status != 0).sum())}
@@ -432,6 +445,8 @@ def main() -> None:
         out[f"tube_{other}"] = tube_leg(dev, other, Bg, steps=min(args.steps, 5), warmup=1)
         out["nominal_ddp"] = {d: nominal_ddp_leg(dev, d, B=4096, steps=args.steps, warmup=args.warmup)
                               for d in ("f32", "f64")}
+        out["nominal_ddp"]["f32_generic"] = nominal_ddp_leg(dev, "f32", B=4096, steps=args.steps,
+                                                            warmup=args.warmup, generic=True)
     if args.dry_run:
         out["dry_run"] = True
     if rank == 0 and not args.no_cpu and world == 1 and not args.dry_run:

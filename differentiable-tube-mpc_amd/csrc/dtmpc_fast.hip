@@ -586,6 +586,8 @@ __device__ __forceinline__ void load_step(StepIn& L, const SV& S, int k) {
 // out (the step's plant and log read the plan's first controls from the records)
 // Rows are read two ahead of their stores (a load waited for right before its own stores would leave
 // one memory latency per row exposed).
+// SHIFT = false (the standalone solve, dtmpc_ilqr_solve_ws): U out as solved.
+template <bool SHIFT = true>
 __device__ __forceinline__ void copy_out(int N, const Rsrc& r, const RA& XA, const RA& UA, const Soa<4>& X,
                                          const Soa<2>& U) {
   const int N1 = N - 1;
@@ -611,13 +613,18 @@ __device__ __forceinline__ void copy_out(int N, const Rsrc& r, const RA& XA, con
       X.st(kk, 3, x.w);
       if (kk < N) {
         const f2 u = uq[j];
-        if (kk > 0) {
-          U.st(kk - 1, 0, u.x);
-          U.st(kk - 1, 1, u.y);
-        }
-        if (kk == N1) {
+        if (!SHIFT) {
           U.st(kk, 0, u.x);
           U.st(kk, 1, u.y);
+        } else {
+          if (kk > 0) {
+            U.st(kk - 1, 0, u.x);
+            U.st(kk - 1, 1, u.y);
+          }
+          if (kk == N1) {
+            U.st(kk, 0, u.x);
+            U.st(kk, 1, u.y);
+          }
         }
       }
     }
@@ -1513,7 +1520,7 @@ constexpr int kSlotInit = 6;   // the initial rollout: bank 1, so the first line
 
 // iLQR for one trajectory (ilqr_traj, core/ddp.py:102-307).  P = 4: no commit pass -- the line search
 // kept every candidate's tape (Slots) and the winner's slot becomes the current tape (S.XA / S.UA).
-template <bool TRACK, int M, int P, class SV>
+template <bool TRACK, int M, int P, bool SHIFT = true, class SV>
 __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const float* x0,
                                     SV& S, int h, const SlotMap& sm, int& iters, Prof& pf, signed char* ch,
                                     size_t chs) {
@@ -1571,7 +1578,7 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
     have_prev = true;
     prev = bestJ;
   }
-  copy_out(p.N, S.r, S.XA, S.UA, S.X, S.U);  // the tape as it stands (a failed solve's too)
+  copy_out<SHIFT>(p.N, S.r, S.XA, S.UA, S.X, S.U);  // the tape as it stands (a failed solve's too)
   return st;
 }
 
@@ -1776,8 +1783,7 @@ __device__ __forceinline__ const char* kargs_ws() { return (const char*)kargs()-
 // the problem constants of one phase; the obstacle table pinned in VGPRs (every candidate of every
 // step reads it; in scalar registers it is what the compiler would spill first)
 template <int M>
-__device__ __forceinline__ FP phase_p() {
-  FP p = kargs()->p;
+__device__ __forceinline__ FP pin_p(FP p) {
 #if DTMPC_FAST_PIN
 #pragma unroll
   for (int j = 0; j < M; ++j) {
@@ -1791,6 +1797,10 @@ __device__ __forceinline__ FP phase_p() {
   }
 #endif
   return p;
+}
+template <int M>
+__device__ __forceinline__ FP phase_p() {
+  return pin_p<M>(kargs()->p);
 }
 
 // GM: 0 general, 1 gamma = 0 gain records, 2 gamma = 0 gain records + Riccati step (the default at gamma = 0)
@@ -1995,6 +2005,7 @@ tube_fast_kernel(FK kk) {
   }
 }
 
+#ifndef DTMPC_FAST_ILQR_TU
 // Known-byte calibration launch for the HBM counters (scripts/pmc_calib.py, rocprofv3 --pmc FETCH_SIZE /
 // WRITE_SIZE): the fast kernel's own access pattern -- per-lane 16-byte X records and 8-byte U records
 // [rows][B][W] through one buffer resource, loaded and stored row by row -- copied from src to dst, so
@@ -2013,11 +2024,172 @@ __global__ void __launch_bounds__(kBlock) record_stream_kernel(const float* src,
     if (k < N) rst2(rd, UA, k, 0, rld2(rs, UA, k, 0));
   }
 }
+#endif
+
+// ---------------------------------------------------------------------------------------------
+// the standalone batched iLQR (dtmpc_ilqr_solve_ws; core/ddp.py:102-307 ilqr_solve) on the fast
+// configuration: the tube step's solver -- the same ilqr() with its lane forms, tape slots and records --
+// run once over a batch of (x0, V_init[, X_ref, U_ref]).  The ABI arrays are the generic kernel's:
+// x0 [4][B], Xref [N+1][3][B], Uref [N][2][B], X [N+1][4][B], U [N][2][B] (in: V_init, out: V*),
+// K [N][8][B] / kff [N][2][B] out (the last backward pass's gains), iters / status [B], choices.
+// Workspace records of one chunk (Bc trajectories): X [N+1][NS][Bc][4], U [N][NS][Bc][2],
+// gains K [N][Bc][8] + k [N][Bc][2], the tracking references XR [N+1][Bc][4] / UR [N][Bc][2].
+struct IArgs {
+  int B, i0, Bc;
+  const float* x0;
+  const float* Xref;
+  const float* Uref;
+  float* X;
+  float* U;
+  float* K;
+  float* kff;
+  int* iters;
+  int* status;
+  signed char* choices;
+  float* work;
+  unsigned wsz, oX, oU, oK, ok, oXR, oUR;
+};
+struct IK {
+  FP p;
+  FCost c;
+  FIlqr cf;
+  IArgs a;
+};
+__device__ __forceinline__ const IK* ikargs() {
+  __attribute__((address_space(4))) const IK* k =
+      (__attribute__((address_space(4))) const IK*)__builtin_amdgcn_kernarg_segment_ptr();
+  __asm__ volatile("" : "+s"(k));
+  return (const IK*)k;
+}
+
+template <int M, int P, bool TRACK, int GM>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+ilqr_fast_kernel(IK kk) {
+  constexpr bool G0 = GM > 0, RG0 = GM > 1;
+  (void)kk;  // read through ikargs()
+  __shared__ f4 lds[DTMPC_FAST_LDS_STEPS > 0 ? kLdsF4 : 1];
+  const IArgs& a = ikargs()->a;
+  const int B = a.B, Bc = a.Bc, i0 = a.i0;
+  const int gl = blockIdx.x * kBlock + threadIdx.x;
+  const int t = gl / P, h = gl % P;
+  const int i = i0 + t;
+  if (t >= Bc) return;
+  const size_t nb = (size_t)B;
+  const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
+  const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
+  constexpr unsigned NS = P == 4 ? kSlots : 1;
+  const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * 8u, l16 = (unsigned)t * 16u, l32 = (unsigned)t * 32u;
+  const SlotMap sm{l16, cb * 16u, l8, cb * 8u};
+  const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * 16u : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * 8u : l8;
+  Solve<TRACK, G0, RG0, P> S;
+  S.r = __builtin_amdgcn_make_buffer_rsrc(a.work, 0, (int)a.wsz, 0x00020000);
+  S.XA = RA{a.oX, NS * cb * 16u, x0lo};
+  S.UA = RA{a.oU, NS * cb * 8u, u0lo};
+  S.XRA = RA{a.oXR, cb * 16u, l16};
+  S.URA = RA{a.oUR, cb * 8u, l8};
+  S.G.L = (lf4*)lds + (threadIdx.x / P);
+  S.G.w = h == 0;
+  S.G.K = RA{a.oK, cb * 32u, l32};
+  S.G.k = RA{a.ok, cb * 8u, l8};
+  S.X = Soa<4>{(char*)a.X, 4u * bb, L};
+  S.U = Soa<2>{(char*)a.U, 2u * bb, L};
+  const FP p = pin_p<M>(ikargs()->p);
+  const int N = p.N;
+  if (TRACK) {  // the references into records (the lanes of a trajectory split the rows; one wave: in order)
+    for (int k = h; k <= N; k += P) {
+      const float* q = a.Xref + (size_t)k * 3 * nb + i;
+      rst4(S.r, S.XRA, k, 0, f4{q[0], q[nb], q[2 * nb], 0.f});
+      if (k < N) {
+        const float* w = a.Uref + (size_t)k * 2 * nb + i;
+        rst2(S.r, S.URA, k, 0, f2{w[0], w[nb]});
+      }
+    }
+  }
+  const float x0[4] = {a.x0[i], a.x0[nb + i], a.x0[2 * nb + i], a.x0[3 * nb + i]};
+  const FCost c = ikargs()->c;
+  const FIlqr cf = ikargs()->cf;
+  signed char* ch = a.choices ? a.choices + i : nullptr;
+  int it = 0;
+  Prof pf;
+  pf.start();
+  const int st = ilqr<TRACK, M, P, false>(p, c, cf, x0, S, h, sm, it, pf, ch, nb);
+  // the last backward pass's gains out to the ABI arrays (G0 records: K's barrier column is exactly 0)
+  for (int k = h; k < N; k += P) {
+    f4 Ka, Kb;
+    f2 kf;
+    S.G.template load<G0>(S.r, k, Ka, Kb, kf);
+    float* Kq = a.K + (size_t)k * 8 * nb + i;
+    Kq[0] = Ka.x;
+    Kq[nb] = Ka.y;
+    Kq[2 * nb] = Ka.z;
+    Kq[3 * nb] = Ka.w;
+    Kq[4 * nb] = Kb.x;
+    Kq[5 * nb] = Kb.y;
+    Kq[6 * nb] = Kb.z;
+    Kq[7 * nb] = Kb.w;
+    float* kq = a.kff + (size_t)k * 2 * nb + i;
+    kq[0] = kf.x;
+    kq[nb] = kf.y;
+  }
+  if (h == 0) {
+    if (a.iters) a.iters[i] = it;
+    a.status[i] |= st;
+  }
+}
 
 }  // namespace fk
 
 // ---------------------------------------------------------------------------------------------
 // host side
+
+static bool fast_spec_ok(const dtmpc_spec* sp) {
+  return sp->obs_aggregation == DTMPC_OBS_SMOOTHMIN && sp->n_obstacles >= 1 && sp->n_obstacles <= 8 &&
+         sp->barrier_type == DTMPC_BARRIER_INVERSE && sp->h_offset == 0.0;
+}
+
+static fk::FIlqr fast_ilqr(const dtmpc_ilqr_cfg& c) {
+  const DIlqr<float> d = make_ilqr<float>(c);
+  fk::FIlqr o;
+  o.max_iter = d.max_iter;
+  o.zpos = d.zpos;
+  o.tol = d.tol;
+  o.reg = d.reg;
+  for (int q = 0; q < fk::NC; ++q) {
+    o.cal[q] = d.calphas[q];
+    o.cpos[q] = d.cpos[q];
+  }
+  return o;
+}
+
+static void fast_p(const dtmpc_spec* sp, fk::FP& p) {
+  const DSpec<float> s = make_spec<float>(*sp);
+  p.N = s.N;
+  p.dt = s.dt;
+  p.umin0 = s.umin0;
+  p.umin1 = s.umin1;
+  p.umax0 = s.umax0;
+  p.umax1 = s.umax1;
+  p.active_tol = s.active_tol;
+  p.neg_beta = s.neg_beta;
+  p.neg_inv_beta = s.neg_inv_beta;
+  p.nbl2e = s.neg_beta * 1.44269504088896341f;
+  p.eps = s.eps;
+  p.gamma = s.gamma;
+  // alpha_eff = max(alpha, eps) and the constants of the relaxed branch, in f32 as the device forms them
+  p.a = s.alpha > s.eps ? s.alpha : s.eps;
+  p.a2 = p.a * p.a;
+  p.a3 = p.a2 * p.a;
+  volatile float one = 1.0f;  // f32 division on the host: correctly rounded, as the device's
+  p.inv_a = one / p.a;
+  p.inv_a2 = one / p.a2;
+  for (int i = 0; i < 8; ++i) {
+    p.cx[i] = i < s.M ? s.cx[i] : 0.f;
+    p.cy[i] = i < s.M ? s.cy[i] : 0.f;
+    p.r2[i] = i < s.M ? s.r2[i] : 0.f;
+  }
+}
+
+#ifndef DTMPC_FAST_ILQR_TU  // the tube step (this file's own translation unit)
 
 // The fast kernel's configuration: f32, smooth-min over 1..8 obstacles, relaxed inverse barrier,
 // untightened h, nominal target cost without wrap, and six rolled-out candidates in both solves.
@@ -2062,58 +2234,17 @@ size_t tube_fast_workspace_bytes(int N, int64_t B, int lanes, int64_t chunk) {
 bool tube_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf) {
   const char* e = getenv("DTMPC_FAST");
   if (e && e[0] == '0' && e[1] == 0) return false;
-  if (dtype != DTMPC_F32) return false;
-  if (sp->obs_aggregation != DTMPC_OBS_SMOOTHMIN || sp->n_obstacles < 1 || sp->n_obstacles > 8) return false;
-  if (sp->barrier_type != DTMPC_BARRIER_INVERSE || sp->h_offset != 0.0) return false;
+  if (dtype != DTMPC_F32 || !fast_spec_ok(sp)) return false;
   if (cf->nominal.kind != DTMPC_COST_TARGET || cf->nominal.wrap_angle) return false;
   const DIlqr<float> n = make_ilqr<float>(cf->nom_ilqr), a = make_ilqr<float>(cf->aux_ilqr);
   return n.nc == fk::NC && a.nc == fk::NC;
-}
-
-static fk::FIlqr fast_ilqr(const dtmpc_ilqr_cfg& c) {
-  const DIlqr<float> d = make_ilqr<float>(c);
-  fk::FIlqr o;
-  o.max_iter = d.max_iter;
-  o.zpos = d.zpos;
-  o.tol = d.tol;
-  o.reg = d.reg;
-  for (int q = 0; q < fk::NC; ++q) {
-    o.cal[q] = d.calphas[q];
-    o.cpos[q] = d.cpos[q];
-  }
-  return o;
 }
 
 int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
                      const dtmpc_tube_state* S, const void* w, hipStream_t st) {
   fk::FK kk;
   std::memset(&kk, 0, sizeof(kk));
-  fk::FP& p = kk.p;
-  const DSpec<float> s = make_spec<float>(*sp);
-  p.N = s.N;
-  p.dt = s.dt;
-  p.umin0 = s.umin0;
-  p.umin1 = s.umin1;
-  p.umax0 = s.umax0;
-  p.umax1 = s.umax1;
-  p.active_tol = s.active_tol;
-  p.neg_beta = s.neg_beta;
-  p.neg_inv_beta = s.neg_inv_beta;
-  p.nbl2e = s.neg_beta * 1.44269504088896341f;
-  p.eps = s.eps;
-  p.gamma = s.gamma;
-  // alpha_eff = max(alpha, eps) and the constants of the relaxed branch, in f32 as the device forms them
-  p.a = s.alpha > s.eps ? s.alpha : s.eps;
-  p.a2 = p.a * p.a;
-  p.a3 = p.a2 * p.a;
-  volatile float one = 1.0f;  // f32 division on the host: correctly rounded, as the device's
-  p.inv_a = one / p.a;
-  p.inv_a2 = one / p.a2;
-  for (int i = 0; i < 8; ++i) {
-    p.cx[i] = i < s.M ? s.cx[i] : 0.f;
-    p.cy[i] = i < s.M ? s.cy[i] : 0.f;
-    p.r2[i] = i < s.M ? s.r2[i] : 0.f;
-  }
+  fast_p(sp, kk.p);
   const DCost<float> c = make_cost<float>(cf->nominal);
   kk.cn = fk::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb, fk::f4{c.t0, c.t1, c.t2, 0.f}};
   kk.cfn = fast_ilqr(cf->nom_ilqr);
@@ -2152,7 +2283,7 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
   // barrier state's zero column (riccati_pk<true>).  DTMPC_FAST_G0 (environment, read at each call) = 0
   // keeps the general records and recursion, = 1 the compact records with the general recursion: the
   // tests compare 1 with 0 for exact equality (records) and the default with the oracle builds.
-  int g0 = p.gamma == 0.f ? 2 : 0;
+  int g0 = kk.p.gamma == 0.f ? 2 : 0;
   if (const char* e = getenv("DTMPC_FAST_G0"))
     if ((e[0] == '0' || e[0] == '1') && e[1] == 0) g0 = g0 < e[0] - '0' ? g0 : e[0] - '0';
   {
@@ -2212,8 +2343,104 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
   return check_launch("tube_fast_kernel");
 }
 
+#else  // the standalone iLQR (csrc/dtmpc_fast_ilqr.hip)
+
+// the standalone solve's records per trajectory: X / U slots, gains K + k, tracking references
+static int64_t ilqr_fast_bytes_per_traj(int N, int lanes) {
+  const int64_t ns = lanes == 4 ? fk::kSlots : 1;
+  return ns * ((int64_t)(N + 1) * 16 + (int64_t)N * 8) + (int64_t)N * 40 + (int64_t)(N + 1) * 16 + (int64_t)N * 8;
+}
+int64_t ilqr_fast_chunk_max(int N, int lanes) {
+  const int64_t c = ((int64_t)0x7fffffff / ilqr_fast_bytes_per_traj(N, lanes)) / kBlock * kBlock;
+  return c < kBlock ? kBlock : c;
+}
+size_t ilqr_fast_workspace_bytes(int N, int64_t B, int lanes) {
+  const int64_t ch = ilqr_fast_chunk_max(N, lanes), b = B < ch ? B : ch;
+  return (size_t)b * (size_t)ilqr_fast_bytes_per_traj(N, lanes);
+}
+
+bool ilqr_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf) {
+  const char* e = getenv("DTMPC_FAST");
+  if (e && e[0] == '0' && e[1] == 0) return false;
+  if (dtype != DTMPC_F32 || !fast_spec_ok(sp) || c->wrap_angle) return false;
+  return make_ilqr<float>(*cf).nc == fk::NC;
+}
+
+int launch_ilqr_fast(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, const void* x0,
+                     const void* Xref, const void* Uref, void* X, void* U, void* K, void* kff, int* iters, int* status,
+                     signed char* choices, int lanes, void* work, size_t work_bytes, hipStream_t st) {
+  const int N = sp->horizon;
+  if (lanes != 1 && lanes != 2 && lanes != 4) return set_err(DTMPC_ERR_BAD_ARG, "lanes must be 1, 2 or 4");
+  if (!work || work_bytes < ilqr_fast_workspace_bytes(N, B, lanes))
+    return set_err(DTMPC_ERR_BAD_ARG, "work_bytes < dtmpc_ilqr_workspace_bytes(...)");
+  fk::IK kk;
+  std::memset(&kk, 0, sizeof(kk));
+  fast_p(sp, kk.p);
+  const DCost<float> c = make_cost<float>(*cp);
+  const bool track = cp->kind == DTMPC_COST_TRACK;
+  kk.c = fk::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb,
+                   track ? fk::f4{0.f, 0.f, 0.f, 0.f} : fk::f4{c.t0, c.t1, c.t2, 0.f}};
+  kk.cf = fast_ilqr(*cf);
+  fk::IArgs& a = kk.a;
+  a.B = (int)B;
+  a.x0 = (const float*)x0;
+  a.Xref = (const float*)Xref;
+  a.Uref = (const float*)Uref;
+  a.X = (float*)X;
+  a.U = (float*)U;
+  a.K = (float*)K;
+  a.kff = (float*)kff;
+  a.iters = iters;
+  a.status = status;
+  a.choices = choices;
+  a.work = (float*)work;
+  // gamma = 0: the compact gain records and the Riccati step without the barrier state's column
+  const int g0 = kk.p.gamma == 0.f ? 2 : 0;
+  const int64_t chunk = ilqr_fast_chunk_max(N, lanes);
+  for (int64_t c0 = 0; c0 < B; c0 += chunk) {
+    const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
+    const int64_t ns = lanes == 4 ? fk::kSlots : 1;
+    a.i0 = (int)c0;
+    a.Bc = (int)Bc;
+    a.oX = 0;
+    a.oU = (unsigned)(ns * Bc * (N + 1) * 16);
+    a.oK = a.oU + (unsigned)(ns * Bc * N * 8);
+    a.ok = a.oK + (unsigned)(Bc * N * 32);
+    a.oXR = a.ok + (unsigned)(Bc * N * 8);
+    a.oUR = a.oXR + (unsigned)(Bc * (N + 1) * 16);
+    a.wsz = a.oUR + (unsigned)(Bc * N * 8);
+    const dim3 grid = grid_for(Bc * lanes);
+#define IL_LAUNCH(m, l, t, g) hipLaunchKernelGGL((fk::ilqr_fast_kernel<m, l, t, g>), grid, dim3(kBlock), 0, st, kk)
+#define IL_G(m, l, t) \
+  if (g0 == 2) IL_LAUNCH(m, l, t, 2); else IL_LAUNCH(m, l, t, 0);
+#define IL_T(m, l) \
+  if (track) { IL_G(m, l, true) } else { IL_G(m, l, false) }
+#define IL_CASE(m) \
+  case m:          \
+    if (lanes == 4) { IL_T(m, 4) } else if (lanes == 2) { IL_T(m, 2) } else { IL_T(m, 1) } break;
+    switch (sp->n_obstacles) {
+#if defined(DTMPC_FAST_M_ONLY)
+      IL_CASE(DTMPC_FAST_M_ONLY)
+#elif defined(DTMPC_FAST_ISA_ONLY)
+      IL_CASE(5)
+#else
+      IL_CASE(1) IL_CASE(2) IL_CASE(3) IL_CASE(4) IL_CASE(5) IL_CASE(6) IL_CASE(7) IL_CASE(8)
+#endif
+      default: return set_err(DTMPC_ERR_BAD_ARG, "fast iLQR: obstacle count not instantiated");
+    }
+#undef IL_CASE
+#undef IL_T
+#undef IL_G
+#undef IL_LAUNCH
+  }
+  return check_launch("ilqr_fast_kernel");
+}
+
+#endif
+
 }  // namespace dtmpc
 
+#ifndef DTMPC_FAST_ILQR_TU
 extern "C" {
 // diagnostics (not part of include/dtmpc.h): the counter-calibration copy of record_stream_kernel over
 // src / dst buffers of (N+1) x 16 + N x 8 bytes per trajectory (< 2^31 bytes)
@@ -2242,3 +2469,4 @@ int dtmpc_prof_lsstat_fast(void* host64) {
 }
 }
 #endif
+#endif  // DTMPC_FAST_ILQR_TU

@@ -175,5 +175,11 @@ int64_t tube_fast_chunk_max(int N, int lanes);
 size_t tube_fast_workspace_bytes(int N, int64_t B, int lanes, int64_t chunk);
 int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
                      const dtmpc_tube_state* S, const void* w, hipStream_t st);
+// the standalone batched iLQR on the same configuration (dtmpc_ilqr_solve_ws)
+bool ilqr_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf);
+size_t ilqr_fast_workspace_bytes(int N, int64_t B, int lanes);
+int launch_ilqr_fast(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, const void* x0,
+                     const void* Xref, const void* Uref, void* X, void* U, void* K, void* kff, int* iters, int* status,
+                     signed char* choices, int lanes, void* work, size_t work_bytes, hipStream_t st);
 
 }  // namespace dtmpc

@@ -649,6 +649,33 @@ int dtmpc_ilqr_solve(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
   return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
 }
 
+size_t dtmpc_ilqr_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t lanes) {
+  if (dtype != DTMPC_F32 && dtype != DTMPC_F64) return 0;
+  if (horizon < 1 || horizon > DTMPC_MAX_HORIZON || B < 1) return 0;
+  if (lanes == 0) lanes = tube_lanes_default(B);
+  if (lanes != 1 && lanes != 2 && lanes != 4) return 0;
+  if (dtype == DTMPC_F64) return 0;  // the generic kernel: no workspace
+  return ilqr_fast_workspace_bytes(horizon, B, lanes);
+}
+
+int dtmpc_ilqr_solve_ws(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
+                        const dtmpc_ilqr_cfg* cfg, int64_t B, const void* x0, const void* Xref,
+                        const void* Uref, void* X, void* U, void* K, void* kff, int32_t* iters,
+                        int32_t* status, int8_t* choices, int32_t lanes, void* work, size_t work_bytes,
+                        void* stream) {
+  int e = check_spec(spec, B);
+  if (e) return e;
+  if ((e = check_cost(cost, Xref, Uref))) return e;
+  if ((e = check_ilqr(cfg))) return e;
+  if (!x0 || !X || !U || !K || !kff || !status) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
+  if (lanes == 0) lanes = tube_lanes_default(B);
+  if (lanes != 1 && lanes != 2 && lanes != 4) return set_err(DTMPC_ERR_BAD_ARG, "lanes must be 0, 1, 2 or 4");
+  if (ilqr_fast_eligible(dtype, spec, cost, cfg))
+    return launch_ilqr_fast(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, (signed char*)choices,
+                            lanes, work, work_bytes, (hipStream_t)stream);
+  return dtmpc_ilqr_solve(dtype, spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, choices, stream);
+}
+
 size_t dtmpc_sensitivity_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t want_lambda) {
   size_t el = dtype == DTMPC_F64 ? 8 : 4;
   size_t per = (size_t)horizon * 20 + (want_lambda ? (size_t)(horizon + 1) * 20 : 0);

@@ -189,6 +189,12 @@ PROTOTYPES = {
         [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, P, P, P, P, P, P, P, P, P, P,
          P],
     ),
+    "dtmpc_ilqr_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64, I32]),
+    "dtmpc_ilqr_solve_ws": (
+        C.c_int,
+        [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, P, P, P, P, P, P, P, P, P, P,
+         I32, P, C.c_size_t, P],
+    ),
     "dtmpc_sensitivity_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64, I32]),
     "dtmpc_ddp_sensitivity": (
         C.c_int,

@@ -225,6 +225,22 @@ int dtmpc_ilqr_solve(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
                      void* K, void* kff, int32_t* iters, int32_t* status, int8_t* choices,
                      void* stream);
 
+/* Workspace bytes of dtmpc_ilqr_solve_ws for B trajectories at `lanes` per trajectory (0: the
+ * dtmpc_tube_lanes(B) default; 1, 2 or 4); 0 for bad arguments and for DTMPC_F64 (generic kernel). */
+size_t dtmpc_ilqr_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t lanes);
+
+/* dtmpc_ilqr_solve (same arrays, same results contract) through the fused solver of the tube step
+ * on the fast configuration -- f32, smooth-min obstacles (1..8), relaxed inverse barrier, h_offset 0,
+ * no angle wrap, six non-zero line-search alphas (plus at most one alpha = 0) -- with `lanes` lanes per
+ * trajectory (0: default) and a caller-owned workspace of dtmpc_ilqr_workspace_bytes; any other
+ * configuration (and DTMPC_FAST=0 in the environment) runs dtmpc_ilqr_solve's generic kernel.
+ * Replaces core/ddp.py:102-307 `ilqr_solve` (the batched nominal DDP of BASELINE config 2). */
+int dtmpc_ilqr_solve_ws(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
+                        const dtmpc_ilqr_cfg* cfg, int64_t B, const void* x0,
+                        const void* Xref, const void* Uref, void* X, void* U,
+                        void* K, void* kff, int32_t* iters, int32_t* status, int8_t* choices,
+                        int32_t lanes, void* work, size_t work_bytes, void* stream);
+
 /* Scratch bytes for dtmpc_ddp_sensitivity. */
 size_t dtmpc_sensitivity_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t want_lambda);
 

@@ -160,6 +160,19 @@ def test_arguments_validated_before_any_device_call(lib):
     rc = lib.dtmpc_tube_step(_abi.F32, C.byref(spec), C.byref(tc), 8, 0, 0, C.byref(state), None, None)
     assert rc == _abi.ERR_BAD_ARG and b"work_bytes" in lib.dtmpc_last_error()
     assert lib.dtmpc_sensitivity_workspace_bytes(_abi.F64, 50, 10, 1) == 8 * 10 * (50 * 20 + 51 * 20)
+    # the standalone fused iLQR: X / U tape slots (12 at four lanes), gains 40 B per step, references
+    ip1, ip4 = (51 * 16 + 50 * 8) + 50 * 40 + 51 * 16 + 50 * 8, 12 * (51 * 16 + 50 * 8) + 50 * 40 + 51 * 16 + 50 * 8
+    assert lib.dtmpc_ilqr_workspace_bytes(_abi.F32, 50, 4096, 4) == ip4 * 4096
+    assert lib.dtmpc_ilqr_workspace_bytes(_abi.F32, 50, 65536, 1) == ip1 * 65536
+    assert lib.dtmpc_ilqr_workspace_bytes(_abi.F32, 50, 1 << 20, 4) == ((0x7FFFFFFF // ip4) // 256 * 256) * ip4
+    assert lib.dtmpc_ilqr_workspace_bytes(_abi.F32, 50, 4096, 3) == 0
+    assert lib.dtmpc_ilqr_workspace_bytes(_abi.F64, 50, 4096, 0) == 0
+    rc = lib.dtmpc_ilqr_solve_ws(_abi.F32, C.byref(spec), C.byref(cost), C.byref(st.ilqr_nom.to_c()), 4, 1, None, None,
+                                 1, 1, 1, 1, None, 1, None, 3, None, 0, None)
+    assert rc == _abi.ERR_BAD_ARG and b"lanes" in lib.dtmpc_last_error()
+    rc = lib.dtmpc_ilqr_solve_ws(_abi.F32, C.byref(spec), C.byref(cost), C.byref(st.ilqr_nom.to_c()), 4, 1, None, None,
+                                 1, 1, 1, 1, None, 1, None, 4, None, 100, None)
+    assert rc == _abi.ERR_BAD_ARG and b"work_bytes" in lib.dtmpc_last_error()
     # the fused episode reset validates before launching
     rc = lib.dtmpc_tube_reset(_abi.F32, C.byref(spec), 8, None, C.byref(state), 1, 1, 1, None)
     assert rc == _abi.ERR_BAD_ARG and b"NULL" in lib.dtmpc_last_error()
