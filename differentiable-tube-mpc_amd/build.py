@@ -2,7 +2,8 @@
 
 Plain hipcc, no build system: the translation units compiled in parallel, then linked --
 csrc/dtmpc_kernels.hip (paper path + per-function entry points), csrc/dtmpc_fast.hip (the fused tube step of
-the paper configuration), csrc/dtmpc_fast_ilqr.hip (its solver as the standalone batched iLQR), csrc/dtmpc_general.hip (general IFT
+the paper configuration), csrc/dtmpc_fast_ilqr.hip (its solver as the standalone batched iLQR), csrc/dtmpc_fast_general.hip (the
+general path's solves on it), csrc/dtmpc_general.hip (general IFT
 path), csrc/dtmpc_receding.hip (receding-horizon nominal MPC driver), csrc/dtmpc_control.hip (tanh-box
 control map + cost derivatives), csrc/dtmpc_ocp.hip (tape cost of core/ocp.py), csrc/dtmpc_systems.hip
 (per-point kernels of the reference's per-function API: dynamics, h, barriers, Jacobians, clamp, cost
@@ -18,10 +19,10 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f)
-        for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_fast_ilqr.hip", "dtmpc_general.hip", "dtmpc_receding.hip",
+        for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_fast_ilqr.hip", "dtmpc_fast_general.hip", "dtmpc_general.hip", "dtmpc_receding.hip",
                   "dtmpc_control.hip", "dtmpc_ocp.hip", "dtmpc_systems.hip")]
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solver.hpp", "dtmpc_general.hpp",
-                                                 "dtmpc_host.hpp", "dtmpc_ls_pk.hpp", "dtmpc_fast.hip")] + [
+                                                 "dtmpc_host.hpp", "dtmpc_ls_pk.hpp")] + [
     os.path.join(os.path.dirname(HERE), "include", h) for h in ("dtmpc.h", "dtmpc_control.h", "dtmpc_systems.h")
 ]
 OUT = os.path.join(HERE, "diff_tube_mpc_strict_pt", "libdtmpc.so")
@@ -38,9 +39,12 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in [*SRCS, *DEPS, __file__])
 
 
+FAST = os.path.join(HERE, "csrc", "dtmpc_fast.hip")  # included by dtmpc_fast_ilqr.hip / dtmpc_fast_general.hip
+
+
 def _key(cmd, src) -> str:
     h = hashlib.sha256(" ".join(cmd).encode())
-    for p in [src, *DEPS]:
+    for p in [src, *DEPS, *([FAST] if os.path.basename(src).startswith("dtmpc_fast") else [])]:
         h.update(open(p, "rb").read())
     return h.hexdigest()[:24]
 

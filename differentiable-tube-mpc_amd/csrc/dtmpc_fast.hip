@@ -25,6 +25,12 @@
 #include "dtmpc_host.hpp"
 #include "dtmpc_ls_pk.hpp"
 
+// this file is the tube step's translation unit; dtmpc_fast_ilqr.hip / dtmpc_fast_general.hip include it
+// for the standalone iLQR's and the general path's instantiations (their host parts below)
+#if defined(DTMPC_FAST_ILQR_TU) || defined(DTMPC_FAST_GENERAL_TU)
+#define DTMPC_FAST_AUX_TU 1
+#endif
+
 namespace dtmpc {
 namespace fk {
 
@@ -44,6 +50,18 @@ struct FP {
   float nbl2e;  // neg_beta * log2(e): exp(-beta h_i - zmax) = exp2(fma(h_i, nbl2e, -zmax log2(e)))
   float a, eps, gamma, inv_a, a2, a3, inv_a2;
   f8 cx, cy, r2;  // ext-vector: SSA values (a float[8] became a private array in memory)
+  float tight;    // h offset of a tightened solve (Obs<M>::tight: the general path's nominal), else unused
+};
+
+// The obstacle template argument M of every h-evaluating function: the obstacle count, with kTight set
+// for a solve whose barrier sees the tightened h - s (core/tube_mpc.py:235-238: the general path's
+// nominal MPC; barrier_dyn(s, h - s.tight) in the generic kernels).  Instantiations without the flag are
+// the tube step's and carry no extra instruction.
+constexpr int kTight = 16;
+template <int M>
+struct Obs {
+  static constexpr int n = M & (kTight - 1);
+  static constexpr bool tight = (M & kTight) != 0;
 };
 
 struct FCost {  // nominal: target; ancillary: tracking (terminal weight = stage weight)
@@ -404,9 +422,10 @@ __device__ __forceinline__ float dbarrier(const FP& p, float z) {
 template <int M, class V>
 __device__ __forceinline__ V h_sm(const FP& p, V px, V py) {
   DTMPC_NOCONTRACT
-  V hi[M], hm;
+  constexpr int MO = Obs<M>::n;
+  V hi[MO], hm;
 #pragma unroll
-  for (int i = 0; i < M; ++i) {
+  for (int i = 0; i < MO; ++i) {
     const V dx = px - p.cx[i];
     const V dy = py - p.cy[i];
     hi[i] = ffma(dx, dx, dy * dy) - p.r2[i];
@@ -416,17 +435,19 @@ __device__ __forceinline__ V h_sm(const FP& p, V px, V py) {
   const V zl = zmax * 1.44269504088896341f;
   V se = 0.f;
 #pragma unroll
-  for (int i = 0; i < M; ++i) se += vexp2(__builtin_elementwise_fma(hi[i], V(p.nbl2e), -zl));
-  return p.neg_inv_beta * (zmax + vlog(se));
+  for (int i = 0; i < MO; ++i) se += vexp2(__builtin_elementwise_fma(hi[i], V(p.nbl2e), -zl));
+  const V hv = p.neg_inv_beta * (zmax + vlog(se));
+  return Obs<M>::tight ? hv - p.tight : hv;  // kTight: the tightened h the barrier sees
 }
 
 // h and grad h at one point (h_grad_fixed, grad_h_multi_circle_obstacles :72-92)
 template <int M>
 __device__ __forceinline__ float h_grad(const FP& p, float px, float py, float& gx, float& gy) {
 #pragma clang fp contract(off)
-  float z[M], hh[M], zmax = 0.f;
+  constexpr int MO = Obs<M>::n;
+  float z[MO], hh[MO], zmax = 0.f;
 #pragma unroll
-  for (int i = 0; i < M; ++i) {
+  for (int i = 0; i < MO; ++i) {
     const float dx = px - p.cx[i];
     const float dy = py - p.cy[i];
     hh[i] = dx * dx + dy * dy - p.r2[i];
@@ -436,7 +457,7 @@ __device__ __forceinline__ float h_grad(const FP& p, float px, float py, float& 
   const float zl = zmax * 1.44269504088896341f;
   float se = 0.f, sx = 0.f, sy = 0.f;
 #pragma unroll
-  for (int i = 0; i < M; ++i) {
+  for (int i = 0; i < MO; ++i) {
     const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(hh[i], p.nbl2e, -zl));
     se += e;
     sx += e * (2.f * (px - p.cx[i]));
@@ -445,6 +466,8 @@ __device__ __forceinline__ float h_grad(const FP& p, float px, float py, float& 
   const float inv = m_rcp(se);
   gx = sx * inv;
   gy = sy * inv;
+  // untightened also under kTight: the reference linearises the nominal with dubins_augmented_jacobian of
+  // the plain h (core/tube_mpc.py:315-320) while its dynamics see h - s (:273-276); dtmpc_solver.hpp alike
   return p.neg_inv_beta * (zmax + m_log(se));
 }
 
@@ -528,11 +551,13 @@ __device__ __forceinline__ V kdot(const f4& K, V e0, V e1, V e2, V e3) {
 
 // ---------------------------------------------------------------------------------------------
 // the tapes one iLQR solve works on
-template <bool TRACK, bool G0, bool RG0, int P>
+template <bool TRACK, bool G0, bool RG0, int P, int NCV = NC>
 struct Solve {
+  static_assert(NCV == NC || (NCV == 4 && P != 4), "four lanes split six candidates");
   static constexpr bool g0 = G0;    // gamma = 0: the compact gain records (Gains)
   static constexpr bool ric0 = RG0; // gamma = 0: the Riccati step without the barrier state's zero column
   static constexpr int lanes = P;   // lanes per trajectory
+  static constexpr int nc = NCV;    // rolled-out line-search candidates (6; the general path's 4 alphas: 4)
   Rsrc r;         // the workspace
   RA XA, UA;      // this solve's tape records (states + barrier state, controls); P = 4: the current slot
   RA XRA, URA;    // TRACK: the nominal plan's records
@@ -1150,9 +1175,10 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
     C.a2[q] = ffma(f2(p.dt), u1[q], C.a2[q]);
   }
   // smooth-min h over the M obstacles (h_sm), all pairs together
-  f2 hi[M][NPR], hm[NPR];
+  constexpr int MO = Obs<M>::n;
+  f2 hi[MO][NPR], hm[NPR];
 #pragma unroll
-  for (int i = 0; i < M; ++i)
+  for (int i = 0; i < MO; ++i)
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
       const f2 dx = C.a0[q] - p.cx[i];
@@ -1167,14 +1193,17 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
     zl[q] = zmax[q] * 1.44269504088896341f;
   }
 #pragma unroll
-  for (int i = 0; i < M; ++i)
+  for (int i = 0; i < MO; ++i)
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
       const f2 e = vexp2(__builtin_elementwise_fma(hi[i][q], f2(p.nbl2e), -zl[q]));
       se[q] = i == 0 ? e : se[q] + e;  // = 0 + e_0 + ...: e_0 >= 0, so 0 + e_0 == e_0 bitwise
     }
 #pragma unroll
-  for (int q = 0; q < NPR; ++q) z[q] = p.neg_inv_beta * (zmax[q] + vlog(se[q]));
+  for (int q = 0; q < NPR; ++q) {
+    z[q] = p.neg_inv_beta * (zmax[q] + vlog(se[q]));
+    if (Obs<M>::tight) z[q] = z[q] - p.tight;
+  }
   // relaxed inverse barrier: the reciprocal for every element, the quadratic branch (z < a) once
   // per step for whichever elements need it
   f2 Bn[NPR];
@@ -1232,7 +1261,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
                                            const SV& S, float Jprev, int h, float& bestJ, float& al_out, int& bc,
                                            const Slots& Z) {
   DTMPC_NOCONTRACT
-  constexpr int NL = P == 4 ? 2 : NC / P;  // candidates of this lane
+  constexpr int NL = P == 4 ? 2 : SV::nc / P;  // candidates of this lane
   constexpr int NPR = (NL + 1) / 2;        // pairs
   const int N = p.N;
   const int hc = P == 4 ? (h < 2 ? h : 2) : h;  // this lane's candidate group
@@ -1379,7 +1408,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   int best = cf.cpos[0];
   al_out = cf.cal[0];
 #pragma unroll
-  for (int a = 1; a < NC; ++a)
+  for (int a = 1; a < SV::nc; ++a)
     if (bi == a) {
       best = cf.cpos[a];
       al_out = cf.cal[a];
@@ -1786,7 +1815,7 @@ template <int M>
 __device__ __forceinline__ FP pin_p(FP p) {
 #if DTMPC_FAST_PIN
 #pragma unroll
-  for (int j = 0; j < M; ++j) {
+  for (int j = 0; j < Obs<M>::n; ++j) {
     float vx = p.cx[j], vy = p.cy[j], vr = p.r2[j];
     __asm__ volatile("" : "+v"(vx));
     __asm__ volatile("" : "+v"(vy));
@@ -2005,7 +2034,7 @@ tube_fast_kernel(FK kk) {
   }
 }
 
-#ifndef DTMPC_FAST_ILQR_TU
+#ifndef DTMPC_FAST_AUX_TU
 // Known-byte calibration launch for the HBM counters (scripts/pmc_calib.py, rocprofv3 --pmc FETCH_SIZE /
 // WRITE_SIZE): the fast kernel's own access pattern -- per-lane 16-byte X records and 8-byte U records
 // [rows][B][W] through one buffer resource, loaded and stored row by row -- copied from src to dst, so
@@ -2137,6 +2166,126 @@ ilqr_fast_kernel(IK kk) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// the general path's two solves (dtmpc_general_step; core/tube_mpc.py:217-392): the nominal MPC with
+// theta-bar (softplus weights, DBaS alpha / gamma from tanh / softplus, the tightened h - s) and the
+// ancillary MPC with theta tracking it, both on the fast solver (general gain records: gamma is a
+// parameter).  The solved tapes go out to the ABI arrays unshifted (dtmpc_general_plant shifts them) and
+// each trajectory's solve status to `sst`; dtmpc_general_step's sensitivity / IFT kernel follows.
+struct GSArgs {
+  int B, i0, Bc;
+  const float* theta;  // [2][12] raw: row 0 ancillary theta, row 1 nominal theta-bar
+  f4 tgt;
+  const float* x;
+  const float* b;
+  const float* xbar;
+  const float* bbar;
+  float* Xnom;
+  float* Unom;
+  float* Xaux;
+  float* Uaux;
+  int* iters;
+  int* sst;
+  float* work;
+  unsigned wsz, oXn, oUn, oXa, oUa, oK, ok;
+};
+struct GSK {
+  FP p;
+  FIlqr cfn, cfa;
+  GSArgs a;
+};
+__device__ __forceinline__ const GSK* gskargs() {
+  __attribute__((address_space(4))) const GSK* k =
+      (__attribute__((address_space(4))) const GSK*)__builtin_amdgcn_kernarg_segment_ptr();
+  __asm__ volatile("" : "+s"(k));
+  return (const GSK*)k;
+}
+
+// the DBaS constants of a parameterised solve, formed in f32 on the device as the generic kernels form
+// them (barrier_relaxed: a = max(alpha, eps), 1 / a and 1 / a^2 correctly rounded)
+__device__ __forceinline__ FP general_fp(FP p, const GPar<float>& g) {
+  DTMPC_NOCONTRACT
+  p.gamma = g.gamma;
+  p.tight = g.tight;
+  p.a = g.alpha > p.eps ? g.alpha : p.eps;
+  p.a2 = p.a * p.a;
+  p.a3 = p.a2 * p.a;
+  p.inv_a = 1.f / p.a;
+  p.inv_a2 = 1.f / p.a2;
+  return p;
+}
+
+template <int M, int P, int NCV>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+general_solve_fast_kernel(GSK kk) {
+  (void)kk;  // read through gskargs()
+  __shared__ f4 lds[1];
+  const GSArgs& a = gskargs()->a;
+  const int B = a.B, Bc = a.Bc, i0 = a.i0;
+  const int gl = blockIdx.x * kBlock + threadIdx.x;
+  const int t = gl / P, h = gl % P;
+  const int i = i0 + t;
+  if (t >= Bc) return;
+  const size_t nb = (size_t)B;
+  const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
+  const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
+  constexpr unsigned NS = P == 4 ? kSlots : 1;
+  const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * 8u, l16 = (unsigned)t * 16u, l32 = (unsigned)t * 32u;
+  const SlotMap sm{l16, cb * 16u, l8, cb * 8u};
+  const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * 16u : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * 8u : l8;
+  Gains<P> G;
+  G.L = (lf4*)lds + (threadIdx.x / P);
+  G.w = h == 0;
+  G.K = RA{a.oK, cb * 32u, l32};
+  G.k = RA{a.ok, cb * 8u, l8};
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc(a.work, 0, (int)a.wsz, 0x00020000);
+  int st = 0, itn = 0, ita = 0;
+  Prof pf;
+  pf.start();
+  Solve<false, false, false, P, NCV> Sn;
+  {  // nominal MPC with theta-bar (:217-291)
+    Sn.r = r;
+    Sn.XA = RA{a.oXn, NS * cb * 16u, x0lo};
+    Sn.UA = RA{a.oUn, NS * cb * 8u, u0lo};
+    Sn.XRA = Sn.XA;
+    Sn.URA = Sn.UA;
+    Sn.G = G;
+    Sn.X = Soa<4>{(char*)a.Xnom, 4u * bb, L};
+    Sn.U = Soa<2>{(char*)a.Unom, 2u * bb, L};
+    const GPar<float> pn = gpar_from<float>(a.theta + DTMPC_P_COUNT, true);
+    const FP p = pin_p<M | kTight>(general_fp(gskargs()->p, pn));
+    const FCost cn{pn.Q[0], pn.Q[1], pn.Q[2], pn.R[0], pn.R[1], pn.Qf[0], pn.Qf[1], pn.Qf[2], pn.qb, a.tgt};
+    const FIlqr cfn = gskargs()->cfn;
+    const float xn0[4] = {a.xbar[i], a.xbar[nb + i], a.xbar[2 * nb + i], a.bbar[i]};
+    st |= ilqr<false, M | kTight, P, false>(p, cn, cfn, xn0, Sn, h, sm, itn, pf, nullptr, 0);
+  }
+  Solve<true, false, false, P, NCV> Sa;
+  {  // ancillary MPC with theta tracking the nominal plan (:296-392)
+    Sa.r = r;
+    Sa.XA = RA{a.oXa, NS * cb * 16u, x0lo};
+    Sa.UA = RA{a.oUa, NS * cb * 8u, u0lo};
+    Sa.XRA = Sn.XA;  // the nominal plan as solved (P = 4: its final slot)
+    Sa.URA = Sn.UA;
+    Sa.G = G;
+    Sa.X = Soa<4>{(char*)a.Xaux, 4u * bb, L};
+    Sa.U = Soa<2>{(char*)a.Uaux, 2u * bb, L};
+    const GPar<float> pa = gpar_from<float>(a.theta, false);
+    const FP p = pin_p<M>(general_fp(gskargs()->p, pa));
+    const FCost ca{pa.Q[0], pa.Q[1], pa.Q[2], pa.R[0], pa.R[1], pa.Qf[0], pa.Qf[1], pa.Qf[2], pa.qb,
+                   f4{0.f, 0.f, 0.f, 0.f}};
+    const FIlqr cfa = gskargs()->cfa;
+    const float xa0[4] = {a.x[i], a.x[nb + i], a.x[2 * nb + i], a.b[i]};
+    st |= ilqr<true, M, P, false>(p, ca, cfa, xa0, Sa, h, sm, ita, pf, nullptr, 0);
+  }
+  if (h == 0) {
+    a.sst[i] = st;
+    if (a.iters) {
+      a.iters[i] = itn;
+      a.iters[nb + i] = ita;
+    }
+  }
+}
+
 }  // namespace fk
 
 // ---------------------------------------------------------------------------------------------
@@ -2189,7 +2338,7 @@ static void fast_p(const dtmpc_spec* sp, fk::FP& p) {
   }
 }
 
-#ifndef DTMPC_FAST_ILQR_TU  // the tube step (this file's own translation unit)
+#ifndef DTMPC_FAST_AUX_TU  // the tube step (this file's own translation unit)
 
 // The fast kernel's configuration: f32, smooth-min over 1..8 obstacles, relaxed inverse barrier,
 // untightened h, nominal target cost without wrap, and six rolled-out candidates in both solves.
@@ -2343,7 +2492,7 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
   return check_launch("tube_fast_kernel");
 }
 
-#else  // the standalone iLQR (csrc/dtmpc_fast_ilqr.hip)
+#elif defined(DTMPC_FAST_ILQR_TU)  // the standalone iLQR (csrc/dtmpc_fast_ilqr.hip)
 
 // the standalone solve's records per trajectory: X / U slots, gains K + k, tracking references
 static int64_t ilqr_fast_bytes_per_traj(int N, int lanes) {
@@ -2436,11 +2585,91 @@ int launch_ilqr_fast(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilq
   return check_launch("ilqr_fast_kernel");
 }
 
+#else  // the general path's solves (csrc/dtmpc_fast_general.hip)
+
+// one lane per trajectory: the records of both solves (two tapes of (N+1) x 16 + N x 8 bytes and the
+// gains' N x 40) fit in the generic scratch of dtmpc_general_workspace_bytes (N x 80 + (N+1) x 40)
+static int64_t general_fast_bytes_per_traj(int N) {
+  return 2 * ((int64_t)(N + 1) * 16 + (int64_t)N * 8) + (int64_t)N * 40;
+}
+
+bool general_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_general_cfg* cf) {
+  const char* e = getenv("DTMPC_FAST");
+  if (e && e[0] == '0' && e[1] == 0) return false;
+  // the tightening s comes from theta-bar (spec.h_offset is not used by the general path)
+  if (dtype != DTMPC_F32 || sp->obs_aggregation != DTMPC_OBS_SMOOTHMIN || sp->n_obstacles < 1 ||
+      sp->n_obstacles > 8 || sp->barrier_type != DTMPC_BARRIER_INVERSE)
+    return false;
+  // six rolled-out candidates (the paper's seven alphas) or four (ILQRConfig's default alphas), the
+  // same list in both solves (check_general)
+  const int nc = make_ilqr<float>(cf->nom_ilqr).nc;
+  return (nc == fk::NC || nc == 4) && make_ilqr<float>(cf->aux_ilqr).nc == nc;
+}
+
+int launch_general_solve_fast(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int64_t B,
+                              const dtmpc_general_state* S, int* sst, hipStream_t st) {
+  const int N = sp->horizon;
+  fk::GSK kk;
+  std::memset(&kk, 0, sizeof(kk));
+  fast_p(sp, kk.p);
+  kk.cfn = fast_ilqr(cf->nom_ilqr);
+  kk.cfa = fast_ilqr(cf->aux_ilqr);
+  fk::GSArgs& a = kk.a;
+  a.B = (int)B;
+  a.theta = (const float*)S->theta;
+  a.tgt = fk::f4{float(cf->target[0]), float(cf->target[1]), float(cf->target[2]), 0.f};
+  a.x = (const float*)S->x;
+  a.b = (const float*)S->b;
+  a.xbar = (const float*)S->xbar;
+  a.bbar = (const float*)S->bbar;
+  a.Xnom = (float*)S->Xnom;
+  a.Unom = (float*)S->Unom;
+  a.Xaux = (float*)S->Xaux;
+  a.Uaux = (float*)S->Uaux;
+  a.iters = S->iters;
+  a.sst = sst;
+  a.work = (float*)S->work;
+  const int nc = make_ilqr<float>(cf->nom_ilqr).nc;
+  const int64_t chunk = ((int64_t)0x7fffffff / general_fast_bytes_per_traj(N)) / kBlock * kBlock;
+  for (int64_t c0 = 0; c0 < B; c0 += chunk) {
+    const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
+    a.i0 = (int)c0;
+    a.Bc = (int)Bc;
+    const unsigned X = (unsigned)(Bc * (N + 1) * 16), U = (unsigned)(Bc * N * 8);
+    a.oXn = 0;
+    a.oXa = X;
+    a.oUn = 2 * X;
+    a.oUa = 2 * X + U;
+    a.oK = 2 * X + 2 * U;
+    a.ok = a.oK + (unsigned)(Bc * N * 32);
+    a.wsz = a.ok + (unsigned)(Bc * N * 8);
+#define GS_LAUNCH(m, n) hipLaunchKernelGGL((fk::general_solve_fast_kernel<m, 1, n>), grid_for(Bc), dim3(kBlock), 0, st, kk)
+#define GS_CASE(m)                 \
+  case m:                          \
+    if (nc == 4) GS_LAUNCH(m, 4);  \
+    else GS_LAUNCH(m, fk::NC);     \
+    break;
+    switch (sp->n_obstacles) {
+#if defined(DTMPC_FAST_M_ONLY)
+      GS_CASE(DTMPC_FAST_M_ONLY)
+#elif defined(DTMPC_FAST_ISA_ONLY)
+      GS_CASE(5)
+#else
+      GS_CASE(1) GS_CASE(2) GS_CASE(3) GS_CASE(4) GS_CASE(5) GS_CASE(6) GS_CASE(7) GS_CASE(8)
+#endif
+      default: return set_err(DTMPC_ERR_BAD_ARG, "fast general solve: obstacle count not instantiated");
+    }
+#undef GS_CASE
+#undef GS_LAUNCH
+  }
+  return check_launch("general_solve_fast_kernel");
+}
+
 #endif
 
 }  // namespace dtmpc
 
-#ifndef DTMPC_FAST_ILQR_TU
+#ifndef DTMPC_FAST_AUX_TU
 extern "C" {
 // diagnostics (not part of include/dtmpc.h): the counter-calibration copy of record_stream_kernel over
 // src / dst buffers of (N+1) x 16 + N x 8 bytes per trajectory (< 2^31 bytes)
@@ -2469,4 +2698,4 @@ int dtmpc_prof_lsstat_fast(void* host64) {
 }
 }
 #endif
-#endif  // DTMPC_FAST_ILQR_TU
+#endif  // DTMPC_FAST_AUX_TU

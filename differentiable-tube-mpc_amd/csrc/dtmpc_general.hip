@@ -122,9 +122,12 @@ struct GenArgs {
   T* gout;         // [25][B] or null
   int* status;
   int* iters;
+  const int* sst;  // SOLVED: the solves' status per trajectory (general_solve_fast_kernel)
 };
 
-template <typename T, int NA>
+// SOLVED: the two solves already ran (the fast solver, general_solve_fast_kernel): the tapes are in
+// Xnom / Unom / Xaux / Uaux and their status in a.sst; this kernel runs the rest of the step.
+template <typename T, int NA, bool SOLVED>
 __global__ void __launch_bounds__(kBlock) general_step_kernel(DSpec<T> s, DIlqr<T> cfn, DIlqr<T> cfa,
                                                               GenArgs<T> a) {
   __shared__ T red[kBlock / 64][DTMPC_GEN_SUMS];
@@ -148,12 +151,16 @@ __global__ void __launch_bounds__(kBlock) general_step_kernel(DSpec<T> s, DIlqr<
     Col<T> none = col<T>((void*)nullptr, i, B);
     int st = 0, itn = 0, ita = 0;
     Prof pr;
-    // nominal MPC with theta-bar (:217-291)
-    T xn0[4] = {a.xbar[i], a.xbar[nb + i], a.xbar[2 * nb + i], a.bbar[i]};
-    st |= ilqr_traj<T, NA>(sn, cn, cfn, xn0, Xn, Un, GainsSoA<T>{K, kf}, none, 0, none, itn, pr, 0);
-    // ancillary MPC with theta tracking the nominal plan (:296-392)
-    T xa0[4] = {a.x[i], a.x[nb + i], a.x[2 * nb + i], a.b[i]};
-    st |= ilqr_traj<T, NA>(sa, ca, cfa, xa0, Xa, Ua, GainsSoA<T>{K, kf}, Xn, 4, Un, ita, pr, 4);
+    if (SOLVED) {
+      st = a.sst[i];
+    } else {
+      // nominal MPC with theta-bar (:217-291)
+      T xn0[4] = {a.xbar[i], a.xbar[nb + i], a.xbar[2 * nb + i], a.bbar[i]};
+      st |= ilqr_traj<T, NA>(sn, cn, cfn, xn0, Xn, Un, GainsSoA<T>{K, kf}, none, 0, none, itn, pr, 0);
+      // ancillary MPC with theta tracking the nominal plan (:296-392)
+      T xa0[4] = {a.x[i], a.x[nb + i], a.x[2 * nb + i], a.b[i]};
+      st |= ilqr_traj<T, NA>(sa, ca, cfa, xa0, Xa, Ua, GainsSoA<T>{K, kf}, Xn, 4, Un, ita, pr, 4);
+    }
     // upper loss L = ||x* - xbar||^2 + ||b*||^2 (:403-408)
     T L1 = T(0), L2 = T(0);
     for (int k = 0; k <= N; ++k) {
@@ -191,7 +198,7 @@ __global__ void __launch_bounds__(kBlock) general_step_kernel(DSpec<T> s, DIlqr<
       for (int j = 0; j < DTMPC_GEN_SUMS; ++j) acc[j] = T(0);
     }
     a.status[i] |= st;
-    if (a.iters) {
+    if (a.iters && !SOLVED) {
       a.iters[i] = itn;
       a.iters[nb + i] = ita;
     }
@@ -387,6 +394,13 @@ __global__ void __launch_bounds__(kBlock) general_plant_kernel(DSpec<T> s, Plant
 // ---------------------------------------------------------------------------------------------
 // host launchers
 
+// the workspace: the generic scratch of the step (N x 20 + (N+1) x 10 values per trajectory; the fast
+// solves' records use its first bytes before the sensitivity does) and the solves' status [B] after it
+static size_t general_scratch_bytes(int dtype, int32_t horizon, int64_t B) {
+  const size_t el = dtype == DTMPC_F64 ? 8 : 4;
+  return (el * ((size_t)horizon * 20 + (size_t)(horizon + 1) * 10) * (size_t)B + 255) / 256 * 256;
+}
+
 template <typename T>
 static int launch_general(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int64_t B,
                           const dtmpc_general_state* S, hipStream_t st) {
@@ -411,10 +425,19 @@ static int launch_general(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int
   a.gout = (T*)S->gout;
   a.status = S->status;
   a.iters = S->iters;
+  const int dtype = sizeof(T) == 4 ? DTMPC_F32 : DTMPC_F64;
+  if (general_fast_eligible(dtype, sp, cf)) {
+    int* sst = (int*)((char*)S->work + general_scratch_bytes(dtype, sp->horizon, B));
+    const int e = launch_general_solve_fast(sp, cf, B, S, sst, st);
+    if (e) return e;
+    a.sst = sst;
+    hipLaunchKernelGGL((general_step_kernel<T, 1, true>), grid_for(B), dim3(kBlock), 0, st, s, cfn, cfa, a);
+    return check_launch("general_step_kernel");
+  }
   switch (cfn.nc) {
 #define CASE(n)                                                                                          \
   case n:                                                                                                \
-    hipLaunchKernelGGL((general_step_kernel<T, n>), grid_for(B), dim3(kBlock), 0, st, s, cfn, cfa, a); \
+    hipLaunchKernelGGL((general_step_kernel<T, n, false>), grid_for(B), dim3(kBlock), 0, st, s, cfn, cfa, a); \
     break;
     DTMPC_NA_CASES(CASE)
 #undef CASE
@@ -539,8 +562,8 @@ int dtmpc_ift_gradient(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost
 int64_t dtmpc_general_partials_count(int64_t B) { return B < 1 ? 0 : (B + kBlock - 1) / kBlock; }
 
 size_t dtmpc_general_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
-  size_t el = dtype == DTMPC_F64 ? 8 : 4;
-  return el * ((size_t)horizon * 20 + (size_t)(horizon + 1) * 10) * (size_t)B;
+  if ((dtype != DTMPC_F32 && dtype != DTMPC_F64) || horizon < 1 || B < 1) return 0;
+  return general_scratch_bytes(dtype, horizon, B) + 4 * (size_t)B;
 }
 
 int dtmpc_general_step(int dtype, const dtmpc_spec* spec, const dtmpc_general_cfg* cfg, int64_t B,
