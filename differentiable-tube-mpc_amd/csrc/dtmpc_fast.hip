@@ -2215,6 +2215,30 @@ __device__ __forceinline__ FP general_fp(FP p, const GPar<float>& g) {
   return p;
 }
 
+// one solve of the general path on its records: G0 when the solve's gamma is exactly 0 (the compact gain
+// records and the Riccati step without the barrier column, as the tube step's default; gamma comes from
+// theta on the device, so the kernel branches -- uniformly -- between the two instantiations).  XA / UA
+// come back as the solved tape's records (P = 4: its final slot).
+template <bool TRACK, int M, int P, int NCV, bool G0>
+__device__ __forceinline__ int general_solve(const FP& p, const FCost& c, const FIlqr& cf, const float* x0, Rsrc r,
+                                             RA& XA, RA& UA, const RA& XRA, const RA& URA, const Gains<P>& G,
+                                             const Soa<4>& X, const Soa<2>& U, int h, const SlotMap& sm, int& it,
+                                             Prof& pf) {
+  Solve<TRACK, G0, G0, P, NCV> S;
+  S.r = r;
+  S.XA = XA;
+  S.UA = UA;
+  S.XRA = XRA;
+  S.URA = URA;
+  S.G = G;
+  S.X = X;
+  S.U = U;
+  const int st = ilqr<TRACK, M, P, false>(p, c, cf, x0, S, h, sm, it, pf, nullptr, 0);
+  XA = S.XA;
+  UA = S.UA;
+  return st;
+}
+
 template <int M, int P, int NCV>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 general_solve_fast_kernel(GSK kk) {
@@ -2242,40 +2266,34 @@ general_solve_fast_kernel(GSK kk) {
   int st = 0, itn = 0, ita = 0;
   Prof pf;
   pf.start();
-  Solve<false, false, false, P, NCV> Sn;
+  RA XN{a.oXn, NS * cb * 16u, x0lo}, UN{a.oUn, NS * cb * 8u, u0lo};
   {  // nominal MPC with theta-bar (:217-291)
-    Sn.r = r;
-    Sn.XA = RA{a.oXn, NS * cb * 16u, x0lo};
-    Sn.UA = RA{a.oUn, NS * cb * 8u, u0lo};
-    Sn.XRA = Sn.XA;
-    Sn.URA = Sn.UA;
-    Sn.G = G;
-    Sn.X = Soa<4>{(char*)a.Xnom, 4u * bb, L};
-    Sn.U = Soa<2>{(char*)a.Unom, 2u * bb, L};
     const GPar<float> pn = gpar_from<float>(a.theta + DTMPC_P_COUNT, true);
     const FP p = pin_p<M | kTight>(general_fp(gskargs()->p, pn));
     const FCost cn{pn.Q[0], pn.Q[1], pn.Q[2], pn.R[0], pn.R[1], pn.Qf[0], pn.Qf[1], pn.Qf[2], pn.qb, a.tgt};
     const FIlqr cfn = gskargs()->cfn;
     const float xn0[4] = {a.xbar[i], a.xbar[nb + i], a.xbar[2 * nb + i], a.bbar[i]};
-    st |= ilqr<false, M | kTight, P, false>(p, cn, cfn, xn0, Sn, h, sm, itn, pf, nullptr, 0);
+    const Soa<4> X{(char*)a.Xnom, 4u * bb, L};
+    const Soa<2> U{(char*)a.Unom, 2u * bb, L};
+    if (pn.gamma == 0.f)
+      st |= general_solve<false, M | kTight, P, NCV, true>(p, cn, cfn, xn0, r, XN, UN, XN, UN, G, X, U, h, sm, itn, pf);
+    else
+      st |= general_solve<false, M | kTight, P, NCV, false>(p, cn, cfn, xn0, r, XN, UN, XN, UN, G, X, U, h, sm, itn, pf);
   }
-  Solve<true, false, false, P, NCV> Sa;
-  {  // ancillary MPC with theta tracking the nominal plan (:296-392)
-    Sa.r = r;
-    Sa.XA = RA{a.oXa, NS * cb * 16u, x0lo};
-    Sa.UA = RA{a.oUa, NS * cb * 8u, u0lo};
-    Sa.XRA = Sn.XA;  // the nominal plan as solved (P = 4: its final slot)
-    Sa.URA = Sn.UA;
-    Sa.G = G;
-    Sa.X = Soa<4>{(char*)a.Xaux, 4u * bb, L};
-    Sa.U = Soa<2>{(char*)a.Uaux, 2u * bb, L};
+  {  // ancillary MPC with theta tracking the nominal plan as solved (:296-392)
+    RA XA{a.oXa, NS * cb * 16u, x0lo}, UA{a.oUa, NS * cb * 8u, u0lo};
     const GPar<float> pa = gpar_from<float>(a.theta, false);
     const FP p = pin_p<M>(general_fp(gskargs()->p, pa));
     const FCost ca{pa.Q[0], pa.Q[1], pa.Q[2], pa.R[0], pa.R[1], pa.Qf[0], pa.Qf[1], pa.Qf[2], pa.qb,
                    f4{0.f, 0.f, 0.f, 0.f}};
     const FIlqr cfa = gskargs()->cfa;
     const float xa0[4] = {a.x[i], a.x[nb + i], a.x[2 * nb + i], a.b[i]};
-    st |= ilqr<true, M, P, false>(p, ca, cfa, xa0, Sa, h, sm, ita, pf, nullptr, 0);
+    const Soa<4> X{(char*)a.Xaux, 4u * bb, L};
+    const Soa<2> U{(char*)a.Uaux, 2u * bb, L};
+    if (pa.gamma == 0.f)
+      st |= general_solve<true, M, P, NCV, true>(p, ca, cfa, xa0, r, XA, UA, XN, UN, G, X, U, h, sm, ita, pf);
+    else
+      st |= general_solve<true, M, P, NCV, false>(p, ca, cfa, xa0, r, XA, UA, XN, UN, G, X, U, h, sm, ita, pf);
   }
   if (h == 0) {
     a.sst[i] = st;
@@ -2285,6 +2303,7 @@ general_solve_fast_kernel(GSK kk) {
     }
   }
 }
+
 
 }  // namespace fk
 
