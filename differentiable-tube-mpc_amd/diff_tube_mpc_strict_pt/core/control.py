@@ -120,12 +120,23 @@ def tanh_box_eval(ctrl: BoxTanhControl, v: Tensor, *, cost: Optional[QuadraticCo
     if cost is not None:
         if x_hat is None:
             raise ValueError("x_hat is required for the cost derivatives")
-        Xs = x_hat.to(v.dtype).reshape(n, 4).t().contiguous()
+        # every per-point operand pairs with v's points: same leading shape (an unbatched one is
+        # broadcast), never a reshape of a different layout with the same element count
+        def per_point(t: Tensor, F: int, name: str) -> Tensor:
+            if t.shape[-1] < F:
+                raise ValueError(f"{name} must have a trailing dimension of at least {F}")
+            if t.shape[:-1] != lead:
+                if t.dim() != 1:
+                    raise ValueError(f"{name} leading shape {tuple(t.shape[:-1])} does not match v's {tuple(lead)}")
+                t = t.expand(*lead, t.shape[-1])
+            return t[..., :F].to(v.dtype).reshape(n, F).t().contiguous()
+
+        Xs = per_point(x_hat, 4, "x_hat")
         if cost.kind == "track":
             if x_ref is None or u_ref is None:
                 raise ValueError("a tracking cost needs x_ref and u_ref")
-            Xr = x_ref[..., :3].to(v.dtype).reshape(n, 3).t().contiguous()
-            Ur = u_ref.to(v.dtype).reshape(n, 2).t().contiguous()
+            Xr = per_point(x_ref, 3, "x_ref")
+            Ur = per_point(u_ref, 2, "u_ref")
         lx = torch.empty(4, n, **kw)
         lv = torch.empty(2, n, **kw)
         lvv = torch.empty(2, n, **kw)

@@ -51,11 +51,24 @@ def total_cost(*, X: Tensor, U: Tensor, cost: QuadraticCost, X_ref: Optional[Ten
     up = (lambda t: t) if batched else (lambda t: None if t is None else t.unsqueeze(0))
     Xb, Ub, Xr, Ur = up(X), up(U), up(X_ref), up(U_ref)
     _require_device(Xb, Ub, Xr, Ur)
+    if Ub.ndim != 3 or Ub.shape[-1] != 2:
+        raise ValueError("U must be [B, N, 2] (or [N, 2])")
     B, N = Ub.shape[0], Ub.shape[1]
     if Xb.shape != (B, N + 1, 4):
         raise ValueError(f"X must be [{B}, {N + 1}, 4]")
-    if cost.kind == "track" and (Xr is None or Ur is None):
-        raise ValueError("a tracking cost needs X_ref and U_ref")
+    if cost.kind == "track":
+        if Xr is None or Ur is None:
+            raise ValueError("a tracking cost needs X_ref and U_ref")
+        # the kernel reads [N+1][3][B] / [N][2][B] references: an unbatched one is broadcast, anything
+        # else must match the batch exactly (never read past a short reference on the device)
+        if Xr.ndim == 3 and Xr.shape[0] == 1 and B > 1:
+            Xr = Xr.expand(B, *Xr.shape[1:])
+        if Ur.ndim == 3 and Ur.shape[0] == 1 and B > 1:
+            Ur = Ur.expand(B, *Ur.shape[1:])
+        if Xr.ndim != 3 or Xr.shape[:2] != (B, N + 1) or Xr.shape[-1] < 3:
+            raise ValueError(f"X_ref must be [{B}, {N + 1}, >=3]")
+        if Ur.shape != (B, N, 2):
+            raise ValueError(f"U_ref must be [{B}, {N}, 2]")
     spec = DubinsDBaSProblem(horizon=N).to_c()
     cc = cost.to_c()
     Xs, Us = to_soa(Xb), to_soa(Ub.to(Xb.dtype))

@@ -5,9 +5,10 @@ against one process running the whole global batch.
 
 Both ranks run on the box's GPUs (rank r on device r mod count).  With two or more devices the sums
 travel over RCCL ("nccl"); on a one-GPU box both ranks share cuda:0 and the sums travel over gloo (RCCL
-refuses two ranks on one device).  f64, fixed iterations: step 0 is per-trajectory bitwise equal (the
-kernel's per-trajectory work does not depend on the shard), theta equal to the single-process update up
-to the order of the batch sum, and identical on both ranks."""
+refuses two ranks on one device).  Fixed iterations, f64 (the generic kernel) and f32 (the fused kernel:
+its chunk-offset partial rows, healthy count and Philox keying by goff + i under sharding): step 0 is
+per-trajectory bitwise equal (the kernel's per-trajectory work does not depend on the shard), theta equal
+to the single-process update up to the order of the batch sum, and identical on both ranks."""
 from __future__ import annotations
 
 import os
@@ -49,10 +50,10 @@ def _x0(lo, hi):
     return torch.from_numpy(x[lo:hi])
 
 
-def _run(lo, hi, dev, group=None):
+def _run(lo, hi, dev, dtype, group=None):
     from diff_tube_mpc_strict_pt.core import TubeMPC
 
-    mpc = TubeMPC(_setup(), batch=hi - lo, device=dev, dtype=torch.float64, disturbance="philox", seed=SEED,
+    mpc = TubeMPC(_setup(), batch=hi - lo, device=dev, dtype=dtype, disturbance="philox", seed=SEED,
                   global_offset=lo, global_batch=B_GLOBAL, process_group=group)
     mpc.reset(_x0(lo, hi))
     xs, ths, sums, sts = [], [], [], []
@@ -66,7 +67,7 @@ def _run(lo, hi, dev, group=None):
     return dict(x=np.stack(xs), th=np.stack(ths), sums=np.stack(sums), status=np.stack(sts), lanes=mpc.lanes)
 
 
-def _worker(rank, world, port, outdir, backend):
+def _worker(rank, world, port, outdir, backend, tag):
     import sys
 
     import torch.distributed as dist
@@ -85,13 +86,14 @@ def _worker(rank, world, port, outdir, backend):
     from diff_tube_mpc_strict_pt.core import shard_range
 
     lo, hi = shard_range(B_GLOBAL, rank, world)
-    r = _run(lo, hi, dev)
+    r = _run(lo, hi, dev, torch.float64 if tag == "f64" else torch.float32)
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), lo=lo, hi=hi, **r)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_sharded_device_loop_matches_single_process(tmp_path, monkeypatch):
+@pytest.mark.parametrize("tag", ["f64", "f32"])
+def test_two_rank_sharded_device_loop_matches_single_process(tmp_path, monkeypatch, tag):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import torch.multiprocessing as mp
@@ -100,9 +102,10 @@ def test_two_rank_sharded_device_loop_matches_single_process(tmp_path, monkeypat
     monkeypatch.setenv("DTMPC_TUBE_LANES", "2")
     world = 2
     backend = "nccl" if torch.cuda.device_count() >= world else "gloo"
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), backend), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), backend, tag), nprocs=world, join=True,
                        start_method="spawn")
-    full = _run(0, B_GLOBAL, torch.device("cuda:0"))
+    f64 = tag == "f64"
+    full = _run(0, B_GLOBAL, torch.device("cuda:0"), torch.float64 if f64 else torch.float32)
     r = [np.load(os.path.join(tmp_path, f"rank{k}.npz")) for k in range(world)]
     assert int(r[0]["hi"]) == int(r[1]["lo"]) and int(r[1]["hi"]) == B_GLOBAL
     assert int(r[0]["lanes"]) == int(r[1]["lanes"]) == int(full["lanes"]) == 2
@@ -110,8 +113,12 @@ def test_two_rank_sharded_device_loop_matches_single_process(tmp_path, monkeypat
         # every rank holds the same theta and the same all-reduced sums
         assert np.array_equal(r[0]["th"][t], r[1]["th"][t]), t
         assert np.array_equal(r[0]["sums"][t], r[1]["sums"][t]), t
-        # healthy count of the whole batch
-        assert r[0]["sums"][t][7] == full["sums"][t][7] == (full["status"][t] == 0).sum(), t
+        # healthy count of the whole batch (f32: status 0 and the gradient within TubeMPC.grad_bound)
+        assert r[0]["sums"][t][7] == full["sums"][t][7], t
+        if f64:
+            assert full["sums"][t][7] == (full["status"][t] == 0).sum(), t
+        else:
+            assert full["sums"][t][7] <= (full["status"][t] == 0).sum(), t
         x_sh = np.concatenate([r[0]["x"][t], r[1]["x"][t]], axis=1)
         st_sh = np.concatenate([r[0]["status"][t], r[1]["status"][t]])
         assert (st_sh == full["status"][t]).mean() > 0.99, t
@@ -120,11 +127,12 @@ def test_two_rank_sharded_device_loop_matches_single_process(tmp_path, monkeypat
             # step 0 reads theta0 only: the shards' kernels compute bit for bit what the whole batch
             # does, and the batch sums / update agree up to the order of the sum over trajectories
             assert np.array_equal(x_sh, full["x"][t])
-            assert np.allclose(r[0]["sums"][t], full["sums"][t], rtol=1e-10, atol=1e-10)
-            assert np.allclose(r[0]["th"][t], full["th"][t], rtol=1e-10, atol=1e-13)
+            tol = 1e-10 if f64 else 2e-5
+            assert np.allclose(r[0]["sums"][t], full["sums"][t], rtol=tol, atol=tol)
+            assert np.allclose(r[0]["th"][t], full["th"][t], rtol=tol, atol=1e-13 if f64 else 1e-7)
         else:
             # later steps run with theta equal up to summation order: per-trajectory states agree
             # within 1e-9 on all but chaotic obstacle-grazing trajectories (whose gradients dominate
             # the batch sums, so those are not compared after step 0)
             err = np.abs(x_sh - full["x"][t]).max(0)
-            assert (err < 1e-9).mean() > 0.99, (t, np.sort(err)[-5:])
+            assert (err < (1e-9 if f64 else 1e-4)).mean() > (0.99 if f64 else 0.97), (t, np.sort(err)[-5:])
