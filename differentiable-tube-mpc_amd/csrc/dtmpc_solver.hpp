@@ -263,16 +263,17 @@ __device__ __forceinline__ void load_step(StepIn<T>& L, const DCost<T>& c, const
 // the alpha = 0 candidate (cfg.zpos) has cost Jprev (the current tape).  Returns the ORIGINAL index
 // of the strictly smallest cost (first wins ties), with its alpha in al_out, or -1 if any candidate is
 // non-finite.
-template <typename T, int NC, typename G>
-__device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg,
-                                           const T* x0, T Bc0, const Col<T>& X, const Col<T>& U,
-                                           const G& gains, const Col<T>& Xr, int rf,
-                                           const Col<T>& Ur, T Jprev, T& bestJ, T& al_out) {
+// The rollouts of NG candidates (alphas al[0..NG)) over the whole horizon, advancing together: their
+// total costs into Jout.
+template <typename T, int NG, typename G>
+__device__ __forceinline__ void ls_rollout(const DSpec<T>& s, const DCost<T>& c, const T* al, const T* x0, T Bc0,
+                                           const Col<T>& X, const Col<T>& U, const G& gains, const Col<T>& Xr,
+                                           int rf, const Col<T>& Ur, T* Jout) {
   DTMPC_NOCONTRACT
   const int N = s.N;
-  T a0[NC], a1[NC], a2[NC], ab[NC], Bc[NC], J[NC];
+  T a0[NG], a1[NG], a2[NG], ab[NG], Bc[NG], J[NG];
 #pragma unroll
-  for (int a = 0; a < NC; ++a) {
+  for (int a = 0; a < NG; ++a) {
     a0[a] = x0[0];
     a1[a] = x0[1];
     a2[a] = x0[2];
@@ -289,28 +290,58 @@ __device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c,
 #pragma unroll
     for (int j = 0; j + 1 < kPrefetch; ++j) q[j] = q[j + 1];
     if (k + kPrefetch < N) load_step(q[kPrefetch - 1], c, X, U, gains, Xr, rf, Ur, k + kPrefetch);
-    T u0[NC], u1[NC];
+    T u0[NG], u1[NG];
 #pragma unroll
-    for (int a = 0; a < NC; ++a) {
+    for (int a = 0; a < NG; ++a) {
       T e0 = a0[a] - cur.X0, e1 = a1[a] - cur.X1, e2 = a2[a] - cur.X2, e3 = ab[a] - cur.X3;
       T du0 = cur.k0 + (cur.K[0] * e0 + cur.K[1] * e1 + cur.K[2] * e2 + cur.K[3] * e3);
       T du1 = cur.k1 + (cur.K[4] * e0 + cur.K[5] * e1 + cur.K[6] * e2 + cur.K[7] * e3);
-      T al = cfg.calphas[a];
-      u0[a] = clampv(cur.V0 + al * du0, s.umin0, s.umax0);
-      u1[a] = clampv(cur.V1 + al * du1, s.umin1, s.umax1);
+      u0[a] = clampv(cur.V0 + al[a] * du0, s.umin0, s.umax0);
+      u1[a] = clampv(cur.V1 + al[a] * du1, s.umin1, s.umax1);
       J[a] = J[a] + stage_cost(c, a0[a], a1[a], a2[a], ab[a], u0[a], u1[a], cur.r0, cur.r1, cur.r2,
                                cur.q0, cur.q1);
     }
-    fhat_vec<T, NC>(s, a0, a1, a2, ab, u0, u1, Bc);
+    fhat_vec<T, NG>(s, a0, a1, a2, ab, u0, u1, Bc);
   }
   T r0, r1, r2;
   load_ref(c, Xr, rf, N, r0, r1, r2);
+#pragma unroll
+  for (int a = 0; a < NG; ++a) Jout[a] = J[a] + term_cost(c, a0[a], a1[a], a2[a], ab[a], r0, r1, r2);
+}
+
+// candidates [C0, NC) in groups of at most GS rollouts (one pass over the step inputs per group)
+template <typename T, int NC, int GS, int C0, typename G>
+__device__ __forceinline__ void ls_groups(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg, const T* x0,
+                                          T Bc0, const Col<T>& X, const Col<T>& U, const G& gains,
+                                          const Col<T>& Xr, int rf, const Col<T>& Ur, T* J) {
+  constexpr int n = NC - C0 < GS ? NC - C0 : GS;
+  T al[n];
+#pragma unroll
+  for (int a = 0; a < n; ++a) al[a] = cfg.calphas[C0 + a];
+  ls_rollout<T, n>(s, c, al, x0, Bc0, X, U, gains, Xr, rf, Ur, J + C0);
+  if constexpr (C0 + n < NC) ls_groups<T, NC, GS, C0 + n>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, J);
+}
+
+// -D DTMPC_LS_GROUPS_F64=1 rolls the f64 candidates out in two groups of three (two passes over the step
+// inputs) instead of six at once.  Measured and kept off (round 3): it cuts the f64 tube kernel's spills
+// from 237 VGPRs to 34 but the step goes 18.6 -> 19.7 ms at B = 65,536 -- the second pass costs more than
+// the scratch traffic it saves.
+#ifndef DTMPC_LS_GROUPS_F64
+#define DTMPC_LS_GROUPS_F64 0
+#endif
+
+template <typename T, int NC, typename G>
+__device__ __forceinline__ int line_search(const DSpec<T>& s, const DCost<T>& c, const DIlqr<T>& cfg,
+                                           const T* x0, T Bc0, const Col<T>& X, const Col<T>& U,
+                                           const G& gains, const Col<T>& Xr, int rf,
+                                           const Col<T>& Ur, T Jprev, T& bestJ, T& al_out) {
+  DTMPC_NOCONTRACT
+  constexpr int GS = (DTMPC_LS_GROUPS_F64 && sizeof(T) == 8 && NC > 3) ? (NC + 1) / 2 : NC;
+  T J[NC];
+  ls_groups<T, NC, GS, 0>(s, c, cfg, x0, Bc0, X, U, gains, Xr, rf, Ur, J);
   bool ok = true;
 #pragma unroll
-  for (int a = 0; a < NC; ++a) {
-    J[a] = J[a] + term_cost(c, a0[a], a1[a], a2[a], ab[a], r0, r1, r2);
-    ok = ok && finite(J[a]);
-  }
+  for (int a = 0; a < NC; ++a) ok = ok && finite(J[a]);
   // first strict minimum among the rolled-out candidates (their relative order is the original one)
   int bc = 0;
   bestJ = J[0];
