@@ -32,11 +32,19 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
 
 
+def _lib_key() -> str:
+    """Content key of the product library: every unit's command line and source texts (not mtimes: a
+    source edited while a build runs must not leave a stale library that looks up to date)."""
+    h = hashlib.sha256(open(__file__, "rb").read())
+    for src in SRCS:
+        h.update(_key([HIPCC, *FLAGS, "-c"], src).encode())
+    return h.hexdigest()
+
+
 def up_to_date() -> bool:
-    if not os.path.exists(OUT):
+    if not os.path.exists(OUT) or not os.path.exists(OUT + ".key"):
         return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(p) <= t for p in [*SRCS, *DEPS, __file__])
+    return open(OUT + ".key").read().strip() == _lib_key()
 
 
 FAST = os.path.join(HERE, "csrc", "dtmpc_fast.hip")  # included by dtmpc_fast_ilqr.hip / dtmpc_fast_general.hip
@@ -58,6 +66,7 @@ def build(force: bool = False, variant: str = "", defines=(), only=()) -> str:
     out = OUT if not variant else OUT.replace("libdtmpc.so", f"libdtmpc_{variant}.so")
     if not variant and not force and up_to_date():
         return out
+    key = _lib_key() if not variant else None  # the sources as they are when the units start compiling
     os.makedirs(CACHE, exist_ok=True)
     objs = []
     procs = []
@@ -82,6 +91,9 @@ def build(force: bool = False, variant: str = "", defines=(), only=()) -> str:
     print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    if key is not None:
+        with open(out + ".key", "w") as f:
+            f.write(key)
     return out
 
 

@@ -1843,7 +1843,7 @@ tube_fast_kernel(FK kk) {
   // the gains of the first steps when DTMPC_FAST_LDS_STEPS > 0 (Gains); the workgroup sums at the end
   __shared__ f4 lds[DTMPC_FAST_LDS_STEPS > 0 ? kLdsF4 : kBlock / 64 * DTMPC_TUBE_SUMS / 4];
   const int B = kargs()->a.B, Bc = kargs()->a.Bc, i0 = kargs()->a.i0;
-  const int gl = blockIdx.x * kBlock + threadIdx.x;
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;  // blockDim: tube_block (64 or 256)
   const int t = gl / P, h = gl % P;  // t: index in the chunk, h: lane of the trajectory
   const int i = i0 + t;              // index in the batch
   float acc[DTMPC_TUBE_SUMS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -2029,8 +2029,8 @@ tube_fast_kernel(FK kk) {
   if (threadIdx.x < DTMPC_TUBE_SUMS) {
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < kBlock / 64; ++q) v += red[q * DTMPC_TUBE_SUMS + threadIdx.x];
-    kargs()->a.partials[((size_t)blockIdx.x + (size_t)i0 * P / kBlock) * DTMPC_TUBE_SUMS + threadIdx.x] = v;
+    for (int q = 0; q < (int)(blockDim.x / 64); ++q) v += red[q * DTMPC_TUBE_SUMS + threadIdx.x];
+    kargs()->a.partials[((size_t)blockIdx.x + (size_t)i0 * P / blockDim.x) * DTMPC_TUBE_SUMS + threadIdx.x] = v;
   }
 }
 
@@ -2099,7 +2099,7 @@ ilqr_fast_kernel(IK kk) {
   __shared__ f4 lds[DTMPC_FAST_LDS_STEPS > 0 ? kLdsF4 : 1];
   const IArgs& a = ikargs()->a;
   const int B = a.B, Bc = a.Bc, i0 = a.i0;
-  const int gl = blockIdx.x * kBlock + threadIdx.x;
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
   const int t = gl / P, h = gl % P;
   const int i = i0 + t;
   if (t >= Bc) return;
@@ -2246,7 +2246,7 @@ general_solve_fast_kernel(GSK kk) {
   __shared__ f4 lds[1];
   const GSArgs& a = gskargs()->a;
   const int B = a.B, Bc = a.Bc, i0 = a.i0;
-  const int gl = blockIdx.x * kBlock + threadIdx.x;
+  const int gl = blockIdx.x * blockDim.x + threadIdx.x;
   const int t = gl / P, h = gl % P;
   const int i = i0 + t;
   if (t >= Bc) return;
@@ -2476,8 +2476,9 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     a.oA8 = f.oA8;
     a.oA2 = f.oA2;
     a.wsz = f.wsz;
-    const dim3 grid = grid_for(Bc * lanes);
-#define FAST_LAUNCH(m, l, g) hipLaunchKernelGGL((fk::tube_fast_kernel<m, l, g>), grid, dim3(kBlock), 0, st, kk)
+    const int bs = tube_block(B, lanes);  // 64 while the batch leaves SIMDs idle: one wave per workgroup
+    const dim3 grid = dim3((unsigned)((Bc * lanes + bs - 1) / bs));
+#define FAST_LAUNCH(m, l, g) hipLaunchKernelGGL((fk::tube_fast_kernel<m, l, g>), grid, dim3(bs), 0, st, kk)
 #define FAST_LANES(m, l) \
   if (g0 == 2) FAST_LAUNCH(m, l, 2); else if (g0) FAST_LAUNCH(m, l, 1); else FAST_LAUNCH(m, l, 0);
 #ifdef DTMPC_FAST_ISA_ONLY  // ISA inspection builds: one instantiation (lanes 1, gamma = 0 records + Riccati)
@@ -2577,8 +2578,9 @@ int launch_ilqr_fast(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilq
     a.oXR = a.ok + (unsigned)(Bc * N * 8);
     a.oUR = a.oXR + (unsigned)(Bc * (N + 1) * 16);
     a.wsz = a.oUR + (unsigned)(Bc * N * 8);
-    const dim3 grid = grid_for(Bc * lanes);
-#define IL_LAUNCH(m, l, t, g) hipLaunchKernelGGL((fk::ilqr_fast_kernel<m, l, t, g>), grid, dim3(kBlock), 0, st, kk)
+    const int bs = tube_block(B, lanes);
+    const dim3 grid = dim3((unsigned)((Bc * lanes + bs - 1) / bs));
+#define IL_LAUNCH(m, l, t, g) hipLaunchKernelGGL((fk::ilqr_fast_kernel<m, l, t, g>), grid, dim3(bs), 0, st, kk)
 #define IL_G(m, l, t) \
   if (g0 == 2) IL_LAUNCH(m, l, t, 2); else IL_LAUNCH(m, l, t, 0);
 #define IL_T(m, l) \
@@ -2649,6 +2651,7 @@ int launch_general_solve_fast(const dtmpc_spec* sp, const dtmpc_general_cfg* cf,
   a.sst = sst;
   a.work = (float*)S->work;
   const int nc = make_ilqr<float>(cf->nom_ilqr).nc;
+  const int bs = tube_block(B, 1);
   const int64_t chunk = ((int64_t)0x7fffffff / general_fast_bytes_per_traj(N)) / kBlock * kBlock;
   for (int64_t c0 = 0; c0 < B; c0 += chunk) {
     const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
@@ -2662,7 +2665,9 @@ int launch_general_solve_fast(const dtmpc_spec* sp, const dtmpc_general_cfg* cf,
     a.oK = 2 * X + 2 * U;
     a.ok = a.oK + (unsigned)(Bc * N * 32);
     a.wsz = a.ok + (unsigned)(Bc * N * 8);
-#define GS_LAUNCH(m, n) hipLaunchKernelGGL((fk::general_solve_fast_kernel<m, 1, n>), grid_for(Bc), dim3(kBlock), 0, st, kk)
+#define GS_LAUNCH(m, n)                                                                                   \
+  hipLaunchKernelGGL((fk::general_solve_fast_kernel<m, 1, n>), dim3((unsigned)((Bc + bs - 1) / bs)), dim3(bs), 0, \
+                     st, kk)
 #define GS_CASE(m)                 \
   case m:                          \
     if (nc == 4) GS_LAUNCH(m, 4);  \

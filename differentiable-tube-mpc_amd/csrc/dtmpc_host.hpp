@@ -168,6 +168,14 @@ inline int check_cost(const dtmpc_cost* c, const void* Xref, const void* Uref) {
 
 inline dim3 grid_for(int64_t B) { return dim3((unsigned)((B + kBlock - 1) / kBlock)); }
 
+// Threads per workgroup of the fused kernels (tube step, standalone iLQR, general solves) for B
+// trajectories at `lanes`: 64 -- one wave per workgroup, so the waves spread over every CU -- while the
+// launch has fewer waves than the device has SIMDs, else 256.  (A 256-thread launch of 4,096 trajectories
+// at four lanes puts its 256 waves on 64 CUs, four per CU, and leaves 192 CUs idle.)  The tube step's
+// partial-sum rows are per workgroup: dtmpc_tube_partials_count follows this rule.
+// -D DTMPC_TUBE_SMALL_BLOCK=0: always 256 (A/B builds).
+int tube_block(int64_t B, int lanes);
+
 // the specialised tube step of the paper configuration (dtmpc_fast.hip)
 bool tube_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf);
 // largest chunk (trajectories per launch) whose per-lane records fit one buffer resource at `lanes`

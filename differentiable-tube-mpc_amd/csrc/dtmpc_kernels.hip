@@ -252,6 +252,13 @@ static int64_t lane_slots() {
   return (int64_t)cus * 4 * 64;
 }
 
+#ifndef DTMPC_TUBE_SMALL_BLOCK
+#define DTMPC_TUBE_SMALL_BLOCK 1
+#endif
+int tube_block(int64_t B, int lanes) {
+  return (DTMPC_TUBE_SMALL_BLOCK && B * lanes < lane_slots()) ? 64 : kBlock;
+}
+
 static int tube_lanes_default(int64_t B) {
   const char* e = getenv("DTMPC_TUBE_LANES");
   if (e && (e[0] == '1' || e[0] == '2' || e[0] == '4') && e[1] == 0) return e[0] - '0';
@@ -523,8 +530,9 @@ static int launch_tube(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B
 #undef CASE
     default: return set_err(DTMPC_ERR_BAD_ARG, "n_alphas out of range");
   }
-  if (S->lanes > lpt) {  // the partial rows past the two-lane grid's: zero, so the reduction of all rows holds
-    const int64_t r0 = (B * lpt + kBlock - 1) / kBlock, r1 = (B * S->lanes + kBlock - 1) / kBlock;
+  {  // the partial rows past this grid's (a 4-lane state, or small-batch 64-thread rows): zero, so the
+     // reduction of all dtmpc_tube_partials_count rows holds
+    const int64_t r0 = (B * lpt + kBlock - 1) / kBlock, r1 = dtmpc_tube_partials_count(B, S->lanes);
     if (r1 > r0 && hipMemsetAsync((T*)S->partials + r0 * DTMPC_TUBE_SUMS, 0, (size_t)(r1 - r0) * DTMPC_TUBE_SUMS * sizeof(T), st) != hipSuccess)
       return check_launch("partials tail");
   }
@@ -751,7 +759,8 @@ int32_t dtmpc_tube_lanes(int64_t B) { return tube_lanes_default(B); }
 
 int64_t dtmpc_tube_partials_count(int64_t B, int32_t lanes) {
   if (B < 1 || (lanes != 1 && lanes != 2 && lanes != 4)) return 0;
-  return (B * lanes + kBlock - 1) / kBlock;
+  const int64_t bs = tube_block(B, lanes);
+  return (B * lanes + bs - 1) / bs;
 }
 
 int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B,

@@ -280,7 +280,8 @@ size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t
  * dtmpc_tube_step never reads the environment. */
 int32_t dtmpc_tube_lanes(int64_t B);
 /* Number of per-workgroup partial records dtmpc_tube_step writes for B trajectories at `lanes`
- * lanes per trajectory (0 if lanes is not a supported count). */
+ * lanes per trajectory (0 if lanes is not a supported count): one per workgroup of 256 threads, or of
+ * 64 threads while B x lanes is below the device's wave slots (CUs x 4 SIMDs x 64). */
 int64_t dtmpc_tube_partials_count(int64_t B, int32_t lanes);
 
 /* One closed-loop step for every trajectory (core/tube_mpc.py:803-1023 loop body):
