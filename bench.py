@@ -234,7 +234,11 @@ def tube_leg(dev, dtype_name: str, B: int, steps: int, warmup: int):
     out = {"batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall,
            "kernel_ms": float(np.mean([a.elapsed_time(b) for a, b in kev])),
            "value": B * ITERS_PER_STEP / wall, "unit": "DDP+IFT iters/s",
-           "flagged_trajectories": int((mpc.status != 0).sum()), "lanes": mpc.lanes}
+           "flagged_trajectories": int((mpc.status != 0).sum()), "lanes": mpc.lanes,
+           # the fused kernel in this precision (f64: csrc/dtmpc_fast64.hip) unless switched off for A/B
+           "kernel": ("generic tube_step_kernel"
+                      if os.environ.get("DTMPC_FAST") == "0" or (dtype_name == "f64" and os.environ.get("DTMPC_FAST64") == "0")
+                      else "fused tube_fast_kernel")}
     del mpc
     torch.cuda.empty_cache()
     return out

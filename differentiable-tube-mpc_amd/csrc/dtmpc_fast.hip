@@ -31,12 +31,36 @@
 #define DTMPC_FAST_AUX_TU 1
 #endif
 
-namespace dtmpc {
-namespace fk {
+// DTMPC_FAST_F64 = 1 (csrc/dtmpc_fast64.hip): the same kernels in f64, the reference's configured precision
+// (configs/dubins.yaml:8) -- `real` is the value type of every tape, record and register, ES its size in
+// 32-bit words (the record strides scale by it); the f64 instantiation lives in namespace fk64 and its host
+// entry points carry the suffix 64 (FKN).  Where the f32 kernel leans on f32-only hardware (v_exp_f32 /
+// v_log_f32 / v_rcp_f32, packed f32, the f32 minimax sin/cos), the f64 form evaluates what the generic
+// f64 kernel evaluates (exp / log / 1/x, the f64 sin/cos of m_sincos).
+#ifndef DTMPC_FAST_F64
+#define DTMPC_FAST_F64 0
+#endif
+#if DTMPC_FAST_F64
+#define FK_NS fk64
+#define FKN(x) x##64
+#else
+#define FK_NS fk
+#define FKN(x) x
+#endif
 
-typedef float f2 __attribute__((ext_vector_type(2)));
-typedef float f4 __attribute__((ext_vector_type(4)));
-typedef float f8 __attribute__((ext_vector_type(8)));
+namespace dtmpc {
+namespace FK_NS {
+
+#if DTMPC_FAST_F64
+typedef double real;
+#else
+typedef float real;
+#endif
+constexpr unsigned ES = sizeof(real) / 4;  // 32-bit words per value: record and SoA byte strides scale by it
+
+typedef real f2 __attribute__((ext_vector_type(2)));
+typedef real f4 __attribute__((ext_vector_type(4)));
+typedef real f8 __attribute__((ext_vector_type(8)));
 typedef int i8v __attribute__((ext_vector_type(8)));
 
 constexpr int NC = 6;  // rolled-out line-search candidates (alpha = 0 is the current tape)
@@ -45,12 +69,12 @@ constexpr int NC = 6;  // rolled-out line-search candidates (alpha = 0 is the cu
 // f32 exactly as the generic kernel forms them on the device (1/a and 1/a^2 correctly rounded).
 struct FP {
   int N;
-  float dt, umin0, umin1, umax0, umax1, active_tol;
-  float neg_beta, neg_inv_beta;
-  float nbl2e;  // neg_beta * log2(e): exp(-beta h_i - zmax) = exp2(fma(h_i, nbl2e, -zmax log2(e)))
-  float a, eps, gamma, inv_a, a2, a3, inv_a2;
-  f8 cx, cy, r2;  // ext-vector: SSA values (a float[8] became a private array in memory)
-  float tight;    // h offset of a tightened solve (Obs<M>::tight: the general path's nominal), else unused
+  real dt, umin0, umin1, umax0, umax1, active_tol;
+  real neg_beta, neg_inv_beta;
+  real nbl2e;  // neg_beta * log2(e): exp(-beta h_i - zmax) = exp2(fma(h_i, nbl2e, -zmax log2(e)))
+  real a, eps, gamma, inv_a, a2, a3, inv_a2;
+  f8 cx, cy, r2;  // ext-vector: SSA values (a real[8] became a private array in memory)
+  real tight;    // h offset of a tightened solve (Obs<M>::tight: the general path's nominal), else unused
 };
 
 // The obstacle template argument M of every h-evaluating function: the obstacle count, with kTight set
@@ -65,13 +89,13 @@ struct Obs {
 };
 
 struct FCost {  // nominal: target; ancillary: tracking (terminal weight = stage weight)
-  float Q0, Q1, Q2, R0, R1, Qf0, Qf1, Qf2, qb;
+  real Q0, Q1, Q2, R0, R1, Qf0, Qf1, Qf2, qb;
   f4 tg;  // target (x, y, theta, -): ext-vector, an SSA value (three floats became a private array)
 };
 
 struct FIlqr {
   int max_iter, zpos;
-  float tol, reg;
+  real tol, reg;
   f8 cal;   // rolled-out candidates' alphas (NC used); ext-vectors: SSA values, never a private array
   i8v cpos; // their original positions
 };
@@ -80,29 +104,29 @@ struct FArgs {
   int B;       // trajectories of the batch: the stride of the ABI SoA arrays
   int i0, Bc;  // this launch's chunk of trajectories [i0, i0 + Bc): the workspace records hold Bc
   long long goff, step;
-  float* x;
-  float* b;
-  float* xbar;
-  float* bbar;
-  float* Xnom;
-  float* Unom;
-  float* Xaux;
-  float* Uaux;
-  float* work;  // workspace: the per-lane records below, one buffer resource (< 2^31 bytes)
+  real* x;
+  real* b;
+  real* xbar;
+  real* bbar;
+  real* Xnom;
+  real* Unom;
+  real* Xaux;
+  real* Uaux;
+  real* work;  // workspace: the per-lane records below, one buffer resource (< 2^31 bytes)
   unsigned wsz;  // bytes of it the records use
   unsigned oXn, oUn, oXa, oUa, oK, ok, oA8, oA2;  // byte offsets of the record arrays in the workspace
-  const float* theta;
-  float* partials;
-  float* log;
+  const real* theta;
+  real* partials;
+  real* log;
   int* status;
   int* iters;
-  const float* w;
+  const real* w;
   int disturbance, write_log;
   unsigned long long seed;
-  float wlo[3], whi[3];
+  real wlo[3], whi[3];
   int stagger;  // s_sleep(127) rounds before this workgroup starts (phase desynchronisation, see launch)
   signed char* choices;  // [nom max_iter + aux max_iter][B] or NULL (dtmpc_tube_state.choices)
-  float gbound;          // health bound on the gradient row (dtmpc_tube_cfg.grad_bound; +inf: none)
+  real gbound;          // health bound on the gradient row (dtmpc_tube_cfg.grad_bound; +inf: none)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -112,13 +136,13 @@ struct FArgs {
 // costs a 64-bit VALU multiply-add per access), the per-lane part a 32-bit byte offset fixed for
 // the whole kernel.
 typedef __attribute__((address_space(1))) char gchar;
-__device__ __forceinline__ float* gaddr(const char* base, size_t row_off, unsigned lane_off) {
+__device__ __forceinline__ real* gaddr(const char* base, size_t row_off, unsigned lane_off) {
   gchar* row = (gchar*)base + row_off;
   __asm__("" : "+s"(row));
   // the lane offset is re-materialised here (volatile: not hoisted out of the step loop), so the
   // zero-extension and the add stay in the access's block and select the scalar-base form
   __asm__ volatile("" : "+v"(lane_off));
-  return (float*)(row + lane_off);
+  return (real*)(row + lane_off);
 }
 
 // a step index known to be wave-uniform (readfirstlane: free when the compiler already keeps it in an
@@ -137,12 +161,12 @@ struct Soa {
   char* base;
   unsigned rs;  // F * B * 4
   Lane L;
-  __device__ __forceinline__ float* p(int k, int f) const {
+  __device__ __forceinline__ real* p(int k, int f) const {
     const unsigned o = f == 0 ? L.f0 : f == 1 ? L.f1 : f == 2 ? L.f2 : L.f3;
     return gaddr(base, (size_t)(unsigned)k * rs, o);
   }
-  __device__ __forceinline__ float ld(int k, int f) const { return *p(k, f); }
-  __device__ __forceinline__ void st(int k, int f, float v) const { *p(k, f) = v; }
+  __device__ __forceinline__ real ld(int k, int f) const { return *p(k, f); }
+  __device__ __forceinline__ void st(int k, int f, real v) const { *p(k, f) = v; }
 };
 
 // per-lane records [rows][B][W] f32 (W = 2 or 8): row k of this lane
@@ -151,15 +175,15 @@ struct Rec {
   char* base;
   unsigned rs;  // B * W * 4
   unsigned lo;  // trajectory * W * 4
-  __device__ __forceinline__ float* p(int k) const {
+  __device__ __forceinline__ real* p(int k) const {
     return gaddr(base, (size_t)(unsigned)k * rs, lo);
   }
 };
 
-__device__ __forceinline__ f4 ld4(const float* q) { return *(const f4*)__builtin_assume_aligned(q, 16); }
-__device__ __forceinline__ f2 ld2(const float* q) { return *(const f2*)__builtin_assume_aligned(q, 8); }
-__device__ __forceinline__ void st4(float* q, f4 v) { *(f4*)__builtin_assume_aligned(q, 16) = v; }
-__device__ __forceinline__ void st2(float* q, f2 v) { *(f2*)__builtin_assume_aligned(q, 8) = v; }
+__device__ __forceinline__ f4 ld4(const real* q) { return *(const f4*)__builtin_assume_aligned(q, 16); }
+__device__ __forceinline__ f2 ld2(const real* q) { return *(const f2*)__builtin_assume_aligned(q, 8); }
+__device__ __forceinline__ void st4(real* q, f4 v) { *(f4*)__builtin_assume_aligned(q, 16) = v; }
+__device__ __forceinline__ void st2(real* q, f2 v) { *(f2*)__builtin_assume_aligned(q, 8) = v; }
 
 // ---------------------------------------------------------------------------------------------
 // the workspace records.  Every per-step array the solver iterates on lives in the workspace as
@@ -181,16 +205,35 @@ struct RA {
   unsigned base, rs, lo;  // uniform base and row stride (bytes), per-lane offset (bytes)
   __device__ __forceinline__ unsigned so(int k) const { return base + (unsigned)k * rs; }
 };
-#ifndef DTMPC_FAST_GLOBAL
+#ifndef DTMPC_FAST_STPOL
+#define DTMPC_FAST_STPOL 0  // cache-policy bits of the record stores (A/B)
+#endif
+#if DTMPC_FAST_F64
+// f64: a 4-value row is 32 bytes (two 16-byte accesses), a 2-value row 16 bytes (one)
+typedef double d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f4 rld4(Rsrc r, const RA& a, int k, unsigned off) {
+  const d2v lo = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off, a.so(k), 0));
+  const d2v hi = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off + 16u, a.so(k), 0));
+  return f4{lo.x, lo.y, hi.x, hi.y};
+}
+__device__ __forceinline__ f2 rld2(Rsrc r, const RA& a, int k, unsigned off) {
+  return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off, a.so(k), 0));
+}
+__device__ __forceinline__ void rst4(Rsrc r, const RA& a, int k, unsigned off, f4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2v{v.x, v.y}), r, a.lo + off, a.so(k), DTMPC_FAST_STPOL);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2v{v.z, v.w}), r, a.lo + off + 16u, a.so(k),
+                                         DTMPC_FAST_STPOL);
+}
+__device__ __forceinline__ void rst2(Rsrc r, const RA& a, int k, unsigned off, f2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, a.lo + off, a.so(k), DTMPC_FAST_STPOL);
+}
+#elif !defined(DTMPC_FAST_GLOBAL)
 __device__ __forceinline__ f4 rld4(Rsrc r, const RA& a, int k, unsigned off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off, a.so(k), 0));
 }
 __device__ __forceinline__ f2 rld2(Rsrc r, const RA& a, int k, unsigned off) {
   return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, a.lo + off, a.so(k), 0));
 }
-#ifndef DTMPC_FAST_STPOL
-#define DTMPC_FAST_STPOL 0  // cache-policy bits of the record stores (A/B)
-#endif
 __device__ __forceinline__ void rst4(Rsrc r, const RA& a, int k, unsigned off, f4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, a.lo + off, a.so(k), DTMPC_FAST_STPOL);
 }
@@ -225,7 +268,7 @@ __device__ __forceinline__ void rst2(Rsrc, const RA& a, int k, unsigned off, f2 
 // -- the step is issue- and latency-bound, not HBM-bound, and a ds_write_b128 costs a wave ~13-26 issue
 // cycles against a buffer store's few; the bytes saved do not buy time.
 typedef __attribute__((address_space(3))) f4 lf4;
-constexpr int kLdsF4 = 163840 / 16;  // 160 KiB: the whole LDS of a CU, one workgroup per CU
+constexpr int kLdsF4 = 163840 / (int)sizeof(f4);  // 160 KiB: the whole LDS of a CU, one workgroup per CU
 
 template <int P, bool G0>
 struct GainLds {
@@ -237,7 +280,7 @@ struct GainLds {
 #ifndef DTMPC_FAST_LDS_STEPS
 #define DTMPC_FAST_LDS_STEPS 0
 #endif
-  static constexpr int KL = !G0 ? 0 : kLdsF4 / (LS * Q) < DTMPC_FAST_LDS_STEPS ? kLdsF4 / (LS * Q) : DTMPC_FAST_LDS_STEPS;
+  static constexpr int KL = (!G0 || DTMPC_FAST_F64) ? 0 : kLdsF4 / (LS * Q) < DTMPC_FAST_LDS_STEPS ? kLdsF4 / (LS * Q) : DTMPC_FAST_LDS_STEPS;
   static constexpr bool used = KL > 0;
 };
 
@@ -250,7 +293,7 @@ struct Gains {
   // so Q_ux's is gamma * S = 0 and K = -Q_uu^-1 Q_ux keeps it), and the iLQR record is the 32 bytes
   // K00 K01 K02 K10 | K11 K12 k0 k1 -- 8 B less per step, two loads instead of three
   template <bool G0>
-  __device__ __forceinline__ void store(Rsrc r, int s, const float* Kk, const float* kk) const {
+  __device__ __forceinline__ void store(Rsrc r, int s, const real* Kk, const real* kk) const {
     using GL = GainLds<P, G0>;
     const f4 g0 = G0 ? f4{Kk[0], Kk[1], Kk[2], Kk[4]} : f4{Kk[0], Kk[1], Kk[2], Kk[3]};
     const f4 g1 = G0 ? f4{Kk[5], Kk[6], kk[0], kk[1]} : f4{Kk[4], Kk[5], Kk[6], Kk[7]};
@@ -262,7 +305,7 @@ struct Gains {
       }
     } else {
       rst4(r, K, s, 0, g0);
-      rst4(r, K, s, 16, g1);
+      rst4(r, K, s, 16 * ES, g1);
       if (!G0) rst2(r, k, s, 0, f2{kk[0], kk[1]});
     }
   }
@@ -281,7 +324,7 @@ struct Gains {
       }
     } else {
       g0 = rld4(r, K, s, 0);
-      g1 = rld4(r, K, s, 16);
+      g1 = rld4(r, K, s, 16 * ES);
       if (!G0) k2 = rld2(r, k, s, 0);
     }
     if (G0) {
@@ -295,29 +338,29 @@ struct Gains {
     }
   }
   // the sensitivity pass's full records K (32 B) + k (8 B), always in the workspace
-  __device__ __forceinline__ void store_full(Rsrc r, int s, const float* Kk, const float* kk) const {
+  __device__ __forceinline__ void store_full(Rsrc r, int s, const real* Kk, const real* kk) const {
     rst4(r, K, s, 0, f4{Kk[0], Kk[1], Kk[2], Kk[3]});
-    rst4(r, K, s, 16, f4{Kk[4], Kk[5], Kk[6], Kk[7]});
+    rst4(r, K, s, 16 * ES, f4{Kk[4], Kk[5], Kk[6], Kk[7]});
     rst2(r, k, s, 0, f2{kk[0], kk[1]});
   }
 };
 
 // ---------------------------------------------------------------------------------------------
-// elementwise math on V = float (one candidate) or f2 (a candidate pair, packed f32 VALU)
+// elementwise math on V = real (one candidate) or f2 (a candidate pair, packed f32 VALU)
 
 template <class V> struct VT;
-template <> struct VT<float> { static constexpr int W = 1; };
+template <> struct VT<real> { static constexpr int W = 1; };
 template <> struct VT<f2> { static constexpr int W = 2; };
 
-__device__ __forceinline__ float vmin(float a, float b) { return m_min(a, b); }
+__device__ __forceinline__ real vmin(real a, real b) { return m_min(a, b); }
 __device__ __forceinline__ f2 vmin(f2 a, f2 b) { return f2{m_min(a.x, b.x), m_min(a.y, b.y)}; }
 // torch.clamp (core/control.py:61-64) as v_maximum3_f32 / v_minimum3_f32: IEEE 754-2019 maximum /
 // minimum propagate NaN like the compare-select form, without a VCC write (no hazard wait states)
-__device__ __forceinline__ float vclamp(float v, float lo, float hi) {
+__device__ __forceinline__ real vclamp(real v, real lo, real hi) {
   return __builtin_elementwise_minimum(__builtin_elementwise_maximum(v, lo), hi);
 }
-__device__ __forceinline__ f2 vclamp(f2 v, float lo, float hi) { return f2{vclamp(v.x, lo, hi), vclamp(v.y, lo, hi)}; }
-__device__ __forceinline__ float vmaxnan(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ f2 vclamp(f2 v, real lo, real hi) { return f2{vclamp(v.x, lo, hi), vclamp(v.y, lo, hi)}; }
+__device__ __forceinline__ real vmaxnan(real a, real b) { return __builtin_elementwise_maximum(a, b); }
 // a * b + c of the forward passes (dynamics, h_i, DBaS update, costs, the commit's u): one fused
 // rounding (v_fma / v_pk_fma; measured 4.66 -> 4.55 ms), the rounding of the oracle's FMA-contraction
 // build; DTMPC_FAST_FWD_FMA=0 rounds twice, as the reference's separate torch ops do.  Written at the
@@ -335,12 +378,88 @@ __device__ __forceinline__ V ffma(V a, V b, V c) {
   return a * b + c;
 #endif
 }
-__device__ __forceinline__ float vexp(float x) { return m_exp(x); }
-__device__ __forceinline__ float vexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+#if DTMPC_FAST_F64
+// f64: exp / log as the generic f64 kernel evaluates them (OCML), the smooth-min terms as it forms them
+// (smterm); sin / cos by a Cody-Waite reduction by pi/2 in three fma steps (the first exact) and the
+// fdlibm kernels __kernel_sin / __kernel_cos on [-pi/4, pi/4] (< 1 ulp), the quadrant applied by exact
+// products with (A, B) in {0, +-1} as in the f32 form; |x| > 2^20 and non-finite take OCML sincos, out of
+// line (its Payne-Hanek branch would otherwise be inlined into every rollout step).
+__device__ __forceinline__ real vexp(real x) { return m_exp(x); }
+__device__ __forceinline__ f2 vexp(f2 x) { return f2{m_exp(x.x), m_exp(x.y)}; }
+__device__ __forceinline__ real vlog(real x) { return m_log(x); }
+__device__ __forceinline__ f2 vlog(f2 x) { return f2{m_log(x.x), m_log(x.y)}; }
+template <class V>
+__device__ __forceinline__ V smterm(const FP& p, V hi, V zmax, V) {
+  DTMPC_NOCONTRACT
+  return vexp(p.neg_beta * hi - zmax);
+}
+#ifndef DTMPC_FAST_SINCOS_AB
+#define DTMPC_FAST_SINCOS_AB 1
+#endif
+constexpr double kDPio2A = 1.5707963267948966, kDPio2B = 6.123233995736766e-17, kDPio2C = -1.4973849048591698e-33,
+                 kD2oPi = 0.6366197723675814;
+constexpr double kDS1 = -1.66666666666666324348e-01, kDS2 = 8.33333333332248946124e-03,
+                 kDS3 = -1.98412698298579493134e-04, kDS4 = 2.75573137070700676789e-06,
+                 kDS5 = -2.50507602534068634195e-08, kDS6 = 1.58969099521155010221e-10;
+constexpr double kDC1 = 4.16666666666666019037e-02, kDC2 = -1.38888888888741095749e-03,
+                 kDC3 = 2.48015872894767294178e-05, kDC4 = -2.75573143513906633035e-07,
+                 kDC5 = 2.08757232129817482790e-09, kDC6 = -1.13596475577881948265e-11;
+#ifndef DTMPC_FAST64_FAR
+#define DTMPC_FAST64_FAR 0  // 0: OCML sincos inline (cold branch), 1: out of line, 2: none (ISA experiments only)
+#endif
+#if DTMPC_FAST64_FAR == 1
+__device__ __attribute__((noinline)) void sincos_far(double x, double* s, double* c) { sincos(x, s, c); }
+#else
+__device__ __forceinline__ void sincos_far(double x, double* s, double* c) { sincos(x, s, c); }
+#endif
+__device__ __forceinline__ void vsincos(real x, real& sn, real& cs) {
+#if DTMPC_FAST64_FAR != 2
+  if (__builtin_expect(!(__builtin_fabs(x) <= 1048576.0), 0)) {
+    sincos_far(x, &sn, &cs);
+    return;
+  }
+#endif
+  const double q = __builtin_rint(x * kD2oPi);
+  double r = __builtin_fma(-q, kDPio2A, x);
+  r = __builtin_fma(-q, kDPio2B, r);
+  r = __builtin_fma(-q, kDPio2C, r);
+  const double z = r * r;
+  double ps = __builtin_fma(z, kDS6, kDS5);
+  ps = __builtin_fma(z, ps, kDS4);
+  ps = __builtin_fma(z, ps, kDS3);
+  ps = __builtin_fma(z, ps, kDS2);
+  const double s = __builtin_fma(z * r, __builtin_fma(z, ps, kDS1), r);
+  double pc = __builtin_fma(z, kDC6, kDC5);
+  pc = __builtin_fma(z, pc, kDC4);
+  pc = __builtin_fma(z, pc, kDC3);
+  pc = __builtin_fma(z, pc, kDC2);
+  pc = __builtin_fma(z, pc, kDC1);
+  const double hz = 0.5 * z, w = 1.0 - hz;
+  const double c = w + (((1.0 - w) - hz) + (z * z) * pc);
+  const double m = __builtin_fma(-4.0, __builtin_floor(__builtin_fma(q, 0.25, 0.25)), q);
+  const double A = 1.0 - __builtin_fabs(m), Bq = __builtin_fmin(m, 2.0 - m);
+  sn = __builtin_fma(s, A, c * Bq);
+  cs = __builtin_fma(c, A, -(s * Bq));
+}
+__device__ __forceinline__ void vsincos(f2 x, f2& s, f2& c) {
+  real s0, c0, s1, c1;
+  vsincos(x.x, s0, c0);
+  vsincos(x.y, s1, c1);
+  s = f2{s0, s1};
+  c = f2{c0, c1};
+}
+#else
+__device__ __forceinline__ real vexp(real x) { return m_exp(x); }
+__device__ __forceinline__ real vexp2(real x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ f2 vexp2(f2 x) { return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; }
 __device__ __forceinline__ f2 vexp(f2 x) { return pk_exp(x); }
-__device__ __forceinline__ float vlog(float x) { return m_log(x); }
+__device__ __forceinline__ real vlog(real x) { return m_log(x); }
 __device__ __forceinline__ f2 vlog(f2 x) { return pk_log(x); }
+// the smooth-min term exp(-beta h_i - zmax) = exp2(fma(h_i, -beta log2(e), -zmax log2(e))) (zl = zmax log2 e)
+template <class V>
+__device__ __forceinline__ V smterm(const FP& p, V hi, V, V zl) {
+  return vexp2(__builtin_elementwise_fma(hi, V(p.nbl2e), -zl));
+}
 // sin / cos for the forward passes: sincos_cw's Cody-Waite reduction x = r + j pi/2 and minimax
 // polynomials, with the quadrant applied WITHOUT selects: sin x = A s + B c, cos x = A c - B s with
 // (A, B) = (cos j pi/2, sin j pi/2) in {0, +-1} -- m = j - 4 floor((j + 1) / 4) in {-1, 0, 1, 2},
@@ -351,29 +470,29 @@ __device__ __forceinline__ f2 vlog(f2 x) { return pk_log(x); }
 #ifndef DTMPC_FAST_SINCOS_AB
 #define DTMPC_FAST_SINCOS_AB 1
 #endif
-__device__ __forceinline__ void sincos_poly(float r, float& s, float& c) {
-  const float z = r * r;
-  float ps = __builtin_fmaf(z, kSinS3, kSinS2);
+__device__ __forceinline__ void sincos_poly(real r, real& s, real& c) {
+  const real z = r * r;
+  real ps = __builtin_fmaf(z, kSinS3, kSinS2);
   ps = __builtin_fmaf(z, ps, kSinS1);
   s = __builtin_fmaf(r * z, ps, r);
-  float pc = __builtin_fmaf(z, kCosK3, kCosK2);
+  real pc = __builtin_fmaf(z, kCosK3, kCosK2);
   pc = __builtin_fmaf(z, pc, kCosK1);
   c = __builtin_fmaf(z * z, pc, __builtin_fmaf(-0.5f, z, 1.0f));
 }
-__device__ __forceinline__ void vsincos(float x, float& sn, float& cs) {
+__device__ __forceinline__ void vsincos(real x, real& sn, real& cs) {
 #if DTMPC_FAST_SINCOS_AB
   if (__builtin_expect(!(__builtin_fabsf(x) <= 65536.0f), 0)) {
     sincosf(x, &sn, &cs);
     return;
   }
-  const float q = __builtin_rintf(x * k2oPi);
-  float r = __builtin_fmaf(-q, kPio2A, x);
+  const real q = __builtin_rintf(x * k2oPi);
+  real r = __builtin_fmaf(-q, kPio2A, x);
   r = __builtin_fmaf(-q, kPio2B, r);
   r = __builtin_fmaf(-q, kPio2C, r);
-  float s, c;
+  real s, c;
   sincos_poly(r, s, c);
-  const float m = __builtin_fmaf(-4.f, __builtin_floorf(__builtin_fmaf(q, 0.25f, 0.25f)), q);
-  const float A = 1.f - __builtin_fabsf(m), Bq = __builtin_fminf(m, 2.f - m);
+  const real m = __builtin_fmaf(-4.f, __builtin_floorf(__builtin_fmaf(q, 0.25f, 0.25f)), q);
+  const real A = 1.f - __builtin_fabsf(m), Bq = __builtin_fminf(m, 2.f - m);
   sn = __builtin_fmaf(s, A, c * Bq);
   cs = __builtin_fmaf(c, A, -(s * Bq));
 #else
@@ -381,21 +500,22 @@ __device__ __forceinline__ void vsincos(float x, float& sn, float& cs) {
 #endif
 }
 __device__ __forceinline__ void vsincos(f2 x, f2& s, f2& c) { pk_sincos(x, s, c); }
-__device__ __forceinline__ bool vfinite(float x) { return finite(x); }
+#endif
+__device__ __forceinline__ bool vfinite(real x) { return finite(x); }
 __device__ __forceinline__ bool vfinite(f2 x) { return finite(x.x) && finite(x.y); }
 
 // relaxed inverse barrier B_alpha (core/barrier.py:36-59) as barrier_relaxed (dtmpc_device.hpp):
 // 1 / max(z, eps) for z >= a; the quadratic extension below a (rare: a trajectory inside an
 // obstacle's margin) is a divergent branch the wave skips when no lane needs it
-__device__ __forceinline__ float bar_relaxed(const FP& p, float z) {
+__device__ __forceinline__ real bar_relaxed(const FP& p, real z) {
   DTMPC_NOCONTRACT
-  const float diff = z - p.a;
+  const real diff = z - p.a;
   return (p.inv_a - diff / p.a2) + (diff * diff) / p.a3;
 }
 // 1 / max(z, eps) with max NaN-propagating (= the reference's torch.clamp_min then reciprocal)
-__device__ __forceinline__ float vbarrier(const FP& p, float z) {
+__device__ __forceinline__ real vbarrier(const FP& p, real z) {
   DTMPC_NOCONTRACT
-  float r = m_rcp(vmaxnan(z, p.eps));
+  real r = m_rcp(vmaxnan(z, p.eps));
   if (!(z >= p.a)) r = bar_relaxed(p, z);
   return r;
 }
@@ -409,12 +529,12 @@ __device__ __forceinline__ f2 vbarrier(const FP& p, f2 z) {
   return r;
 }
 // _dB_relaxed_inv_dz core/systems/dubins_aug_jac.py:31-40 (dbarrier_relaxed)
-__device__ __forceinline__ float dbarrier(const FP& p, float z) {
+__device__ __forceinline__ real dbarrier(const FP& p, real z) {
   if (z >= p.a) {
-    const float zc = z < p.eps ? p.eps : z;
+    const real zc = z < p.eps ? p.eps : z;
     return -m_rcp(zc * zc);
   }
-  const float diff = z - p.a;
+  const real diff = z - p.a;
   return -p.inv_a2 + (2.f * diff) / p.a3;
 }
 
@@ -432,38 +552,44 @@ __device__ __forceinline__ V h_sm(const FP& p, V px, V py) {
     hm = i == 0 ? hi[0] : vmin(hm, hi[i]);
   }
   const V zmax = p.neg_beta * hm;
-  const V zl = zmax * 1.44269504088896341f;
+  const V zl = zmax * real(1.44269504088896341);
   V se = 0.f;
 #pragma unroll
-  for (int i = 0; i < MO; ++i) se += vexp2(__builtin_elementwise_fma(hi[i], V(p.nbl2e), -zl));
+  for (int i = 0; i < MO; ++i) se += smterm(p, hi[i], zmax, zl);
   const V hv = p.neg_inv_beta * (zmax + vlog(se));
   return Obs<M>::tight ? hv - p.tight : hv;  // kTight: the tightened h the barrier sees
 }
 
 // h and grad h at one point (h_grad_fixed, grad_h_multi_circle_obstacles :72-92)
 template <int M>
-__device__ __forceinline__ float h_grad(const FP& p, float px, float py, float& gx, float& gy) {
+__device__ __forceinline__ real h_grad(const FP& p, real px, real py, real& gx, real& gy) {
 #pragma clang fp contract(off)
   constexpr int MO = Obs<M>::n;
-  float z[MO], hh[MO], zmax = 0.f;
+  real z[MO], hh[MO], zmax = 0.f;
 #pragma unroll
   for (int i = 0; i < MO; ++i) {
-    const float dx = px - p.cx[i];
-    const float dy = py - p.cy[i];
+    const real dx = px - p.cx[i];
+    const real dy = py - p.cy[i];
     hh[i] = dx * dx + dy * dy - p.r2[i];
     z[i] = p.neg_beta * hh[i];
     zmax = (i == 0 || z[i] > zmax) ? z[i] : zmax;
   }
-  const float zl = zmax * 1.44269504088896341f;
-  float se = 0.f, sx = 0.f, sy = 0.f;
+#if !DTMPC_FAST_F64
+  const real zl = zmax * real(1.44269504088896341);
+#endif
+  real se = 0.f, sx = 0.f, sy = 0.f;
 #pragma unroll
   for (int i = 0; i < MO; ++i) {
-    const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(hh[i], p.nbl2e, -zl));
+#if DTMPC_FAST_F64
+    const real e = m_exp(z[i] - zmax);  // the generic kernel's h_grad (dtmpc_device.hpp)
+#else
+    const real e = __builtin_amdgcn_exp2f(__builtin_fmaf(hh[i], p.nbl2e, -zl));
+#endif
     se += e;
     sx += e * (2.f * (px - p.cx[i]));
     sy += e * (2.f * (py - p.cy[i]));
   }
-  const float inv = m_rcp(se);
+  const real inv = m_rcp(se);
   gx = sx * inv;
   gy = sy * inv;
   // untightened also under kTight: the reference linearises the nominal with dubins_augmented_jacobian of
@@ -490,15 +616,15 @@ __device__ __forceinline__ void fhat(const FP& p, V& x0, V& x1, V& x2, V& b, V u
 }
 
 template <int M>
-__device__ __forceinline__ float barrier_at(const FP& p, float px, float py) {
+__device__ __forceinline__ real barrier_at(const FP& p, real px, real py) {
   return vbarrier(p, h_sm<M>(p, px, py));
 }
 
 // stage / terminal cost (stage_cost / term_cost, core/tube_mpc.py:823-842, 875-894): TRACK takes the
 // references r (state) and q (control), the nominal its fixed target
 template <bool TRACK, class V>
-__device__ __forceinline__ V stage(const FCost& c, V x0, V x1, V x2, V b, V u0, V u1, float r0, float r1, float r2,
-                                   float q0, float q1) {
+__device__ __forceinline__ V stage(const FCost& c, V x0, V x1, V x2, V b, V u0, V u1, real r0, real r1, real r2,
+                                   real q0, real q1) {
   DTMPC_NOCONTRACT
   V d0, d1, d2, e0, e1;
   if (TRACK) {
@@ -519,7 +645,7 @@ __device__ __forceinline__ V stage(const FCost& c, V x0, V x1, V x2, V b, V u0, 
   return ffma(V(c.qb), b * b, sq + sr);
 }
 template <bool TRACK, class V>
-__device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, float r0, float r1, float r2) {
+__device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, real r0, real r1, real r2) {
   DTMPC_NOCONTRACT
   V d0, d1, d2;
   if (TRACK) {
@@ -573,7 +699,7 @@ struct Solve {
 };
 
 struct StepIn {
-  float X0, X1, X2, X3, V0, V1, r0, r1, r2, q0, q1;
+  real X0, X1, X2, X3, V0, V1, r0, r1, r2, q0, q1;
   f4 Ka, Kb;
   f2 kk;
 };
@@ -659,15 +785,15 @@ __device__ __forceinline__ void copy_out(int N, const Rsrc& r, const RA& XA, con
 // iLQR start (init_tape): V = clamp(V_init) (the warm start, ABI SoA), X = rollout(x0, V) into this
 // solve's records, and the alpha = 0 candidate's cost
 template <bool TRACK, int M, class SV>
-__device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const float* x0, const SV& S,
+__device__ __forceinline__ real init_tape(const FP& p, const FCost& c, const real* x0, const SV& S,
                                            bool want_cost) {
   DTMPC_NOCONTRACT
   const int N = p.N;
-  float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3];
-  float Bc = barrier_at<M>(p, x0[0], x0[1]);
+  real s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3];
+  real Bc = barrier_at<M>(p, x0[0], x0[1]);
   S.stx(0, f4{s0, s1, s2, sb});
-  float J = 0.f;
-  float n0 = S.U.ld(0, 0), n1 = S.U.ld(0, 1);
+  real J = 0.f;
+  real n0 = S.U.ld(0, 0), n1 = S.U.ld(0, 1);
   f4 nR = f4{0.f, 0.f, 0.f, 0.f};
   f2 nQ = f2{0.f, 0.f};
   if (TRACK) {
@@ -675,7 +801,7 @@ __device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const fl
     nQ = S.ur(0);
   }
   for (int k = 0; k < N; ++k) {
-    const float v0 = n0, v1 = n1;
+    const real v0 = n0, v1 = n1;
     const f4 R = nR;
     const f2 Q = nQ;
     if (k + 1 < N) {
@@ -686,7 +812,7 @@ __device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const fl
         nQ = S.ur(k + 1);
       }
     }
-    const float u0 = vclamp(v0, p.umin0, p.umax0), u1 = vclamp(v1, p.umin1, p.umax1);
+    const real u0 = vclamp(v0, p.umin0, p.umax0), u1 = vclamp(v1, p.umin1, p.umax1);
     S.stu(k, f2{u0, u1});
     if (want_cost) J = J + stage<TRACK>(c, s0, s1, s2, sb, u0, u1, R.x, R.y, R.z, Q.x, Q.y);
     fhat<M, SV::g0>(p, s0, s1, s2, sb, u0, u1, Bc);
@@ -699,17 +825,17 @@ __device__ __forceinline__ float init_tape(const FP& p, const FCost& c, const fl
 }
 
 // sparse augmented Jacobian (make_jac, core/systems/dubins_aug_jac.py:61-139)
-__device__ __forceinline__ Jac<float> jac(const FP& p, float sn, float cs, float v, float gxk, float gyk, float dBk,
-                                          float gxn, float gyn, float dBn) {
-  Jac<float> J;
-  const float dt = p.dt;
+__device__ __forceinline__ Jac<real> jac(const FP& p, real sn, real cs, real v, real gxk, real gyk, real dBk,
+                                          real gxn, real gyn, real dBn) {
+  Jac<real> J;
+  const real dt = p.dt;
   J.a02 = -dt * v * sn;
   J.a12 = dt * v * cs;
   J.b00 = dt * cs;
   J.b10 = dt * sn;
   J.b21 = dt;
-  const float r0 = dBn * gxn, r1 = dBn * gyn, r2 = dBn * 0.f;
-  const float gd = p.gamma * dBk;
+  const real r0 = dBn * gxn, r1 = dBn * gyn, r2 = dBn * 0.f;
+  const real gd = p.gamma * dBk;
   J.a30 = r0 - gd * gxk;
   J.a31 = r1 - gd * gyk;
   J.a32 = (r0 * J.a02 + r1 * J.a12 + r2) - gd * 0.f;
@@ -734,7 +860,7 @@ struct RicP {
   f2 Vx[2];    // (V_x0, V_x1), (V_x2, V_x3)
 };
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 bc(float v) { return f2{v, v}; }
+__device__ __forceinline__ f2 bc(real v) { return f2{v, v}; }
 
 // G0 (gamma = 0): A's column for the barrier state is exactly zero, so the recursion keeps V_xx's row /
 // column 3 at (0, 0, 0, 2 q_b) and V_x[3] at l_x[3] = 2 q_b b (the terms it would add are products with
@@ -743,21 +869,21 @@ __device__ __forceinline__ f2 bc(float v) { return f2{v, v}; }
 // contracts two of them differently (l_u1 + b21 V_x2 and l_uu1 + s2 b21 become one fma each): an FMA
 // rounding of the same recursion, checked against the oracle builds like the rest of the kernel.
 template <bool G0>
-__device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx, const float* lu, const float* lxx,
-                                           const float* luu, float reg, RicP& R, float* K, float* kff) {
-  const float a02 = J.a02, a12 = J.a12, a30 = J.a30, a31 = J.a31, a32 = J.a32, g = J.g;
-  const float b00 = J.b00, b10 = J.b10, b21 = J.b21, b30 = J.b30, b31 = J.b31;
+__device__ __forceinline__ bool riccati_pk(const Jac<real>& J, const real* lx, const real* lu, const real* lxx,
+                                           const real* luu, real reg, RicP& R, real* K, real* kff) {
+  const real a02 = J.a02, a12 = J.a12, a30 = J.a30, a31 = J.a31, a32 = J.a32, g = J.g;
+  const real b00 = J.b00, b10 = J.b10, b21 = J.b21, b30 = J.b30, b31 = J.b31;
   const f2 A3 = f2{a30, a31};
-  const float vx0 = R.Vx[0].x, vx1 = R.Vx[0].y, vx2 = R.Vx[1].x, vx3 = R.Vx[1].y;
+  const real vx0 = R.Vx[0].x, vx1 = R.Vx[0].y, vx2 = R.Vx[1].x, vx3 = R.Vx[1].y;
   // G0: V_xx row 3 = (0, 0 | 0, 2 q_b)
   const f2 V30 = G0 ? f2{0.f, 0.f} : R.V[3][0];
   const f2 V31 = G0 ? f2{0.f, lxx[3]} : R.V[3][1];
   // Q_x = l_x + A^T V_x ; Q_u = l_u + B^T V_x
   const f2 Qx01 = f2{lx[0], lx[1]} + fma2(A3, bc(vx3), R.Vx[0]);
-  const float Qx2 = lx[2] + (a02 * vx0 + a12 * vx1 + vx2 + a32 * vx3);
-  const float Qx3 = G0 ? lx[3] : lx[3] + g * vx3;
-  const float Qu0 = lu[0] + (b00 * vx0 + b10 * vx1 + b30 * vx3);
-  const float Qu1 = G0 ? lu[1] + b21 * vx2 : lu[1] + (b21 * vx2 + b31 * vx3);
+  const real Qx2 = lx[2] + (a02 * vx0 + a12 * vx1 + vx2 + a32 * vx3);
+  const real Qx3 = G0 ? lx[3] : lx[3] + g * vx3;
+  const real Qu0 = lu[0] + (b00 * vx0 + b10 * vx1 + b30 * vx3);
+  const real Qu1 = G0 ? lu[1] + b21 * vx2 : lu[1] + (b21 * vx2 + b31 * vx3);
   // P = A^T V_xx
   f2 P[4][2];
   if (G0) {
@@ -782,7 +908,7 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
   f2 Q[4][2];
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
-    const float p0 = P[i][0].x, p1 = P[i][0].y, p2 = P[i][1].x, p3 = P[i][1].y;
+    const real p0 = P[i][0].x, p1 = P[i][0].y, p2 = P[i][1].x, p3 = P[i][1].y;
     Q[i][0] = fma2(A3, bc(p3), P[i][0]);
     Q[i][1] = f2{a02 * p0 + a12 * p1 + p2 + a32 * p3, G0 ? 0.f : g * p3};
   }
@@ -811,10 +937,10 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
     }
   }
   f2 Qux[2][2];
-  float Quu[2][2];
+  real Quu[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
-    const float s0 = S[a][0].x, s1 = S[a][0].y, s2 = S[a][1].x, s3 = S[a][1].y;
+    const real s0 = S[a][0].x, s1 = S[a][0].y, s2 = S[a][1].x, s3 = S[a][1].y;
     Qux[a][0] = fma2(A3, bc(s3), S[a][0]);
     Qux[a][1] = f2{a02 * s0 + a12 * s1 + s2 + a32 * s3, G0 ? 0.f : g * s3};
     Quu[a][0] = s0 * b00 + s1 * b10 + s3 * b30;
@@ -823,7 +949,7 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
   Quu[0][0] = luu[0] + Quu[0][0];
   Quu[1][1] = luu[1] + Quu[1][1];
   // gains with the regularised Q_uu (:239-249): LU with partial pivoting, K = -x, k = -x
-  const LU2<float> f = lu2(Quu[0][0] + reg, Quu[0][1], Quu[1][0], Quu[1][1] + reg);
+  const LU2<real> f = lu2(Quu[0][0] + reg, Quu[0][1], Quu[1][0], Quu[1][1] + reg);
   f2 Kp[2][2];  // K row a, columns (0, 1) and (2, 3)
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
@@ -834,8 +960,8 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
     Kp[0][c] = (p0 + bc(f.a01) * Kp[1][c]) * bc(-f.inv00);
   }
   {
-    const float p0 = f.sw ? Qu1 : Qu0, p1 = f.sw ? Qu0 : Qu1;
-    const float y1 = p1 - f.l * p0;
+    const real p0 = f.sw ? Qu1 : Qu0, p1 = f.sw ? Qu0 : Qu1;
+    const real y1 = p1 - f.l * p0;
     kff[1] = y1 * -f.inv11;
     kff[0] = (p0 + f.a01 * kff[1]) * -f.inv00;
   }
@@ -869,9 +995,9 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
     const int ci = i >> 1;
-    const float kq0 = (i & 1) ? KQ0[ci].y : KQ0[ci].x, kq1 = (i & 1) ? KQ1[ci].y : KQ1[ci].x;
-    const float k0i = (i & 1) ? Kp[0][ci].y : Kp[0][ci].x, k1i = (i & 1) ? Kp[1][ci].y : Kp[1][ci].x;
-    const float q0i = (i & 1) ? Qux[0][ci].y : Qux[0][ci].x, q1i = (i & 1) ? Qux[1][ci].y : Qux[1][ci].x;
+    const real kq0 = (i & 1) ? KQ0[ci].y : KQ0[ci].x, kq1 = (i & 1) ? KQ1[ci].y : KQ1[ci].x;
+    const real k0i = (i & 1) ? Kp[0][ci].y : Kp[0][ci].x, k1i = (i & 1) ? Kp[1][ci].y : Kp[1][ci].x;
+    const real q0i = (i & 1) ? Qux[0][ci].y : Qux[0][ci].x, q1i = (i & 1) ? Qux[1][ci].y : Qux[1][ci].x;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       f2 acc = fma2(bc(kq0), Kp[0][c], Q[i][c]);
@@ -885,15 +1011,28 @@ __device__ __forceinline__ bool riccati_pk(const Jac<float>& J, const float* lx,
   return ok;
 }
 
+// one DPP move of a real (f64: both 32-bit halves with the same control)
+template <int C>
+__device__ __forceinline__ real dpp_mov(real v) {
+#if DTMPC_FAST_F64
+  typedef int i2v __attribute__((ext_vector_type(2)));
+  const i2v w = __builtin_bit_cast(i2v, v);
+  return __builtin_bit_cast(real, i2v{__builtin_amdgcn_mov_dpp(w.x, C, 0xF, 0xF, false),
+                                      __builtin_amdgcn_mov_dpp(w.y, C, 0xF, 0xF, false)});
+#else
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), C, 0xF, 0xF, false));
+#endif
+}
+
 // broadcast of lane J of each group of P lanes (P = 2: quad_perm [J, J, J+2, J+2]; P = 4: [J, J, J, J]),
 // one DPP move; j is a constant after unrolling
 template <int P, int J>
-__device__ __forceinline__ float gbc(float v) {
+__device__ __forceinline__ real gbc(real v) {
   constexpr int ctrl = P == 4 ? J * 0x55 : (J == 0 ? 0xA0 : 0xF5);
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false));
+  return dpp_mov<ctrl>(v);
 }
 template <int P>
-__device__ __forceinline__ float gbcast(float v, int j) {
+__device__ __forceinline__ real gbcast(real v, int j) {
   switch (j) {
     case 0: return gbc<P, 0>(v);
     case 1: return gbc<P, 1 % P>(v);
@@ -904,7 +1043,7 @@ __device__ __forceinline__ float gbcast(float v, int j) {
 
 // the per-point part of the linearisation: sin / cos of the heading, grad h and B'(h) at X
 struct Lin {
-  float sn, cs, gx, gy, dB;
+  real sn, cs, gx, gy, dB;
 };
 template <int M>
 __device__ __forceinline__ Lin lin_point(const FP& p, const f4& X) {
@@ -920,15 +1059,15 @@ __device__ __forceinline__ Lin lin_point(const FP& p, const f4& X) {
 // and runs on every lane (each needs the gains).  Same operations on the same values as P = 1: the
 // gains are bitwise those of the one-lane form.
 template <bool TRACK, int M, class SV>
-__device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg, const SV& S, int h) {
+__device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, const SV& S, int h) {
   constexpr int P = SV::lanes;
   const int N = p.N;
-  const float lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
-  const float luu[2] = {2.f * c.R0, 2.f * c.R1};
-  const float pxx[4] = {2.f * c.Qf0, 2.f * c.Qf1, 2.f * c.Qf2, 2.f * c.qb};
+  const real lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
+  const real luu[2] = {2.f * c.R0, 2.f * c.R1};
+  const real pxx[4] = {2.f * c.Qf0, 2.f * c.Qf1, 2.f * c.Qf2, 2.f * c.qb};
   const f4 XN = S.x(N);
-  const float xn0 = XN.x, xn1 = XN.y, xn2 = XN.z, xnb = XN.w;
-  float d0, d1, d2;
+  const real xn0 = XN.x, xn1 = XN.y, xn2 = XN.z, xnb = XN.w;
+  real d0, d1, d2;
   if (TRACK) {
     const f4 RN = S.xr(N);
     d0 = xn0 - RN.x;
@@ -953,7 +1092,7 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
   R.Vx[1] = f2{pxx[2] * d2, pxx[3] * xnb};
 #define RVX(i) ((i) == 0 ? R.Vx[0].x : (i) == 1 ? R.Vx[0].y : (i) == 2 ? R.Vx[1].x : R.Vx[1].y)
 #else
-  Riccati<float> R;
+  Riccati<real> R;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -964,8 +1103,8 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
   R.Vx[3] = pxx[3] * xnb;
 #define RVX(i) (R.Vx[i])
 #endif
-  float gxn, gyn;
-  float dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
+  real gxn, gyn;
+  real dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
   bool ok = finite(RVX(0)) && finite(RVX(1)) && finite(RVX(2)) && finite(RVX(3));
   // step inputs one step ahead
   f4 nX = S.x(N - 1), nR = f4{0.f, 0.f, 0.f, 0.f};
@@ -975,8 +1114,8 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
     nQ = S.ur(N - 1);
   }
   auto step = [&](const f4& X, const f2& V, const f4& Rr, const f2& Q, int k, const Lin& Lk) {
-    const float x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w, u0 = V.x, u1 = V.y;
-    const Jac<float> J = jac(p, Lk.sn, Lk.cs, u0, Lk.gx, Lk.gy, Lk.dB, gxn, gyn, dBn);
+    const real x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w, u0 = V.x, u1 = V.y;
+    const Jac<real> J = jac(p, Lk.sn, Lk.cs, u0, Lk.gx, Lk.gy, Lk.dB, gxn, gyn, dBn);
     if (TRACK) {
       d0 = x0 - Rr.x;
       d1 = x1 - Rr.y;
@@ -986,8 +1125,8 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
       d1 = x1 - c.tg.y;
       d2 = x2 - c.tg.z;
     }
-    const float lx[4] = {lxx[0] * d0, lxx[1] * d1, lxx[2] * d2, lxx[3] * xb};
-    float lu[2];
+    const real lx[4] = {lxx[0] * d0, lxx[1] * d1, lxx[2] * d2, lxx[3] * xb};
+    real lu[2];
     if (TRACK) {
       lu[0] = luu[0] * (u0 - Q.x);
       lu[1] = luu[1] * (u1 - Q.y);
@@ -995,7 +1134,7 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
       lu[0] = luu[0] * u0;
       lu[1] = luu[1] * u1;
     }
-    float Kk[8], kk[2];
+    real Kk[8], kk[2];
 #if DTMPC_FAST_RICPK
     ok = riccati_pk<SV::ric0>(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
 #else
@@ -1067,7 +1206,10 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, float reg,
 // ops / compare-select sits back to back (each such pair costs an s_nop wait state on gfx950).
 // Arithmetic per candidate is the scalar forward pass (fhat, stage) operation for operation.
 #ifndef DTMPC_FAST_LS_DEPTH2
-#define DTMPC_FAST_LS_DEPTH2 1  // two steps of prefetch lead (one lane per trajectory: measured -1.5 %)
+// two steps of prefetch lead (f32, one lane per trajectory: measured -1.5 %).  f64: one -- the four step
+// buffers of 21 doubles would not fit beside the candidates (at one lane: 380 scratch spill / reload
+// instructions in the kernel, 23 with two buffers)
+#define DTMPC_FAST_LS_DEPTH2 (DTMPC_FAST_F64 ? 0 : 1)
 #endif
 template <int NPR>
 struct Cand {
@@ -1077,7 +1219,12 @@ struct Cand {
 // sin / cos of NPR pairs (pk_sincos per pair); one range test for all of them
 template <int NPR>
 __device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
-  float m = __builtin_fabsf(x[0].x);
+#if DTMPC_FAST_F64
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) vsincos(x[q], sn[q], cs[q]);
+}
+#else
+  real m = __builtin_fabsf(x[0].x);
 #pragma unroll
   for (int q = 0; q < NPR; ++q) m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(x[q].x), __builtin_fabsf(x[q].y)));
 #ifndef DTMPC_OCML_SINCOS
@@ -1121,8 +1268,8 @@ __device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
       const int j0 = (int)qq[q].x & 3, j1 = (int)qq[q].y & 3;
-      const float so0 = (j0 & 1) ? c[q].x : s[q].x, co0 = (j0 & 1) ? s[q].x : c[q].x;
-      const float so1 = (j1 & 1) ? c[q].y : s[q].y, co1 = (j1 & 1) ? s[q].y : c[q].y;
+      const real so0 = (j0 & 1) ? c[q].x : s[q].x, co0 = (j0 & 1) ? s[q].x : c[q].x;
+      const real so1 = (j1 & 1) ? c[q].y : s[q].y, co1 = (j1 & 1) ? s[q].y : c[q].y;
       sn[q] = f2{(j0 & 2) ? -so0 : so0, (j1 & 2) ? -so1 : so1};
       cs[q] = f2{((j0 + 1) & 2) ? -co0 : co0, ((j1 + 1) & 2) ? -co1 : co1};
     }
@@ -1132,13 +1279,14 @@ __device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
 #endif
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {  // some element out of range: each element as the scalar form
-    float s0, c0, s1, c1;
+    real s0, c0, s1, c1;
     vsincos(x[q].x, s0, c0);
     vsincos(x[q].y, s1, c1);
     sn[q] = f2{s0, s1};
     cs[q] = f2{c0, c1};
   }
 }
+#endif
 
 // one step of the NPR pairs' rollouts: feedback + clamp, stage cost, DBaS-augmented Dubins move
 template <bool TRACK, int M, int NPR, bool G0>
@@ -1190,13 +1338,13 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
     zmax[q] = p.neg_beta * hm[q];
-    zl[q] = zmax[q] * 1.44269504088896341f;
+    zl[q] = zmax[q] * real(1.44269504088896341);
   }
 #pragma unroll
   for (int i = 0; i < MO; ++i)
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
-      const f2 e = vexp2(__builtin_elementwise_fma(hi[i][q], f2(p.nbl2e), -zl[q]));
+      const f2 e = smterm(p, hi[i][q], zmax[q], zl[q]);
       se[q] = i == 0 ? e : se[q] + e;  // = 0 + e_0 + ...: e_0 >= 0, so 0 + e_0 == e_0 bitwise
     }
 #pragma unroll
@@ -1207,11 +1355,11 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
   // relaxed inverse barrier: the reciprocal for every element, the quadratic branch (z < a) once
   // per step for whichever elements need it
   f2 Bn[NPR];
-  float zmin = z[0].x;
+  real zmin = z[0].x;
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
     Bn[q] = f2{m_rcp(vmaxnan(z[q].x, p.eps)), m_rcp(vmaxnan(z[q].y, p.eps))};
-    zmin = __builtin_fminf(zmin, __builtin_fminf(z[q].x, z[q].y));
+    zmin = m_min(zmin, m_min(z[q].x, z[q].y));
   }
   if (!(zmin >= p.a)) {
 #pragma unroll
@@ -1245,8 +1393,8 @@ __device__ __forceinline__ T pick3(int h, T a, T b, T c) { return h == 0 ? a : h
 
 // the partner of this lane in a lane group at distance 1 (quad_perm [1, 0, 3, 2]) or 2 ([2, 3, 0, 1])
 template <int D>
-__device__ __forceinline__ float gswap(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), D == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false));
+__device__ __forceinline__ real gswap(real v) {
+  return dpp_mov<D == 1 ? 0xB1 : 0x4E>(v);
 }
 template <int D>
 __device__ __forceinline__ int gswap(int v) { return __builtin_amdgcn_mov_dpp(v, D == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false); }
@@ -1257,8 +1405,8 @@ __device__ __forceinline__ int gswap(int v) { return __builtin_amdgcn_mov_dpp(v,
 // P = 4: one pair per lane (lane 3 repeats lane 2's), each lane storing its pair's tapes (Slots).  The
 // lanes of a trajectory combine their minima by DPP swaps.
 template <bool TRACK, int M, int P, class SV>
-__device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FIlqr& cf, const float* x0, float Bc0,
-                                           const SV& S, float Jprev, int h, float& bestJ, float& al_out, int& bc,
+__device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FIlqr& cf, const real* x0, real Bc0,
+                                           const SV& S, real Jprev, int h, real& bestJ, real& al_out, int& bc,
                                            const Slots& Z) {
   DTMPC_NOCONTRACT
   constexpr int NL = P == 4 ? 2 : SV::nc / P;  // candidates of this lane
@@ -1339,14 +1487,14 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
     }
   }
   }
-  float r0 = 0.f, r1 = 0.f, r2 = 0.f;
+  real r0 = 0.f, r1 = 0.f, r2 = 0.f;
   if (TRACK) {
     const f4 RN = S.xr(N);
     r0 = RN.x;
     r1 = RN.y;
     r2 = RN.z;
   }
-  float Jc[2 * NPR];
+  real Jc[2 * NPR];
   bool ok = true;
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
@@ -1356,7 +1504,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
     ok = ok && vfinite(Jt);
   }
   // this lane's first strict minimum (its candidates are in increasing original order)
-  float bJ = Jc[0];
+  real bJ = Jc[0];
   int bl = 0;
 #pragma unroll
   for (int a = 1; a < NL; ++a)
@@ -1366,7 +1514,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
     }
   int bi = c0 + bl;  // index into the candidate list (its order is the original one)
   // the zero candidate's neighbours: min over candidates before / after its position
-  float mb = 0.f, ma = 0.f;
+  real mb = 0.f, ma = 0.f;
   int hb = 0, ha = 0;
   if (cf.zpos >= 0) {
 #pragma unroll
@@ -1385,7 +1533,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   }
   // combine with the trajectory's other lanes: lexicographic (J, position) = strict <, first wins
   auto combine = [&](auto sw) {
-    const float oJ = sw(bJ);
+    const real oJ = sw(bJ);
     const int oi = sw(bi);
     ok = sw((int)ok) && ok;
     if (oJ < bJ || (oJ == bJ && oi < bi)) {
@@ -1393,7 +1541,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
       bi = oi;
     }
     if (cf.zpos >= 0) {
-      const float omb = sw(mb), oma = sw(ma);
+      const real omb = sw(mb), oma = sw(ma);
       const int ohb = sw(hb), oha = sw(ha);
       if (ohb) mb = (!hb || omb < mb) ? omb : mb;
       if (oha) ma = (!ha || oma < ma) ? oma : ma;
@@ -1437,14 +1585,14 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
 // materialise the chosen candidate in place (commit_candidate): same arithmetic as its lane of the
 // line search; the old X[k+1] is read (prefetched) before it is overwritten
 template <bool TRACK, int M, class SV>
-__device__ __forceinline__ void commit(const FP& p, float al, const float* x0, float Bc0, const SV& S) {
+__device__ __forceinline__ void commit(const FP& p, real al, const real* x0, real Bc0, const SV& S) {
   DTMPC_NOCONTRACT
   const int N = p.N;
-  float s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bc = Bc0;
+  real s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bc = Bc0;
 #if DTMPC_FAST_CM_RECOMP
   // the tape's X is rollout(x0, U) by this same scalar fhat (init_tape, commit), so re-rolling the old
   // controls reproduces the old X bit for bit and saves its 16 B per step of HBM reads
-  float o0 = s0, o1 = s1, o2 = s2, ob = sb, Bo = Bc0;
+  real o0 = s0, o1 = s1, o2 = s2, ob = sb, Bo = Bc0;
   constexpr bool LX = false;
 #else
   constexpr bool LX = true;
@@ -1456,20 +1604,20 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
   T0.G = S.G;
   auto step = [&](const StepIn& cur, int k) {
 #if DTMPC_FAST_CM_RECOMP
-    const float e0 = s0 - o0, e1 = s1 - o1, e2 = s2 - o2, e3 = sb - ob;
+    const real e0 = s0 - o0, e1 = s1 - o1, e2 = s2 - o2, e3 = sb - ob;
     fhat<M>(p, o0, o1, o2, ob, cur.V0, cur.V1, Bo);
 #else
-    const float e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
+    const real e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
 #endif
 #if DTMPC_FAST_KFMA
-    const float du0 = cur.kk.x + kdot<SV::g0>(cur.Ka, e0, e1, e2, e3);
-    const float du1 = cur.kk.y + kdot<SV::g0>(cur.Kb, e0, e1, e2, e3);
+    const real du0 = cur.kk.x + kdot<SV::g0>(cur.Ka, e0, e1, e2, e3);
+    const real du1 = cur.kk.y + kdot<SV::g0>(cur.Kb, e0, e1, e2, e3);
 #else
-    const float du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
-    const float du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
+    const real du0 = cur.kk.x + (cur.Ka.x * e0 + cur.Ka.y * e1 + cur.Ka.z * e2 + cur.Ka.w * e3);
+    const real du1 = cur.kk.y + (cur.Kb.x * e0 + cur.Kb.y * e1 + cur.Kb.z * e2 + cur.Kb.w * e3);
 #endif
-    const float u0 = vclamp(ffma(al, du0, cur.V0), p.umin0, p.umax0);
-    const float u1 = vclamp(ffma(al, du1, cur.V1), p.umin1, p.umax1);
+    const real u0 = vclamp(ffma(al, du0, cur.V0), p.umin0, p.umax0);
+    const real u1 = vclamp(ffma(al, du1, cur.V1), p.umin1, p.umax1);
 #ifdef DTMPC_FAST_DIAG_NOSTORE  // timing attribution only: the commit computes but stores nothing
     fhat<M>(p, s0, s1, s2, sb, u0, u1, Bc);
     if (__builtin_isnan(s0 + u0 + u1)) S.stx(k + 1, f4{s0, s1, s2, sb});
@@ -1521,7 +1669,7 @@ __device__ __forceinline__ void commit(const FP& p, float al, const float* x0, f
 // each: [0..7] winners by original alpha position (lanes), [8] wave-iterations, [9] waves where every
 // lane keeps its tape (alpha = 0), [10] every lane takes the first alpha, [11] every lane one of the two
 __device__ unsigned long long g_lsstat[64];
-__device__ __forceinline__ void ls_stat(int trk, int best, float al, const FIlqr& cf) {
+__device__ __forceinline__ void ls_stat(int trk, int best, real al, const FIlqr& cf) {
   unsigned long long* g = g_lsstat + 32 * trk;
   const bool lead = (threadIdx.x & 63) == (__builtin_ctzll(__ballot(1)));
 #pragma unroll
@@ -1550,16 +1698,16 @@ constexpr int kSlotInit = 6;   // the initial rollout: bank 1, so the first line
 // iLQR for one trajectory (ilqr_traj, core/ddp.py:102-307).  P = 4: no commit pass -- the line search
 // kept every candidate's tape (Slots) and the winner's slot becomes the current tape (S.XA / S.UA).
 template <bool TRACK, int M, int P, bool SHIFT = true, class SV>
-__device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const float* x0,
+__device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const real* x0,
                                     SV& S, int h, const SlotMap& sm, int& iters, Prof& pf, signed char* ch,
                                     size_t chs) {
   constexpr int ph = TRACK ? 4 : 0;  // phase-timer slots (profiling builds)
   if (ch && h == 0)  // the decision record: -1 for iterations not run (dtmpc_tube_state.choices)
     for (int it = 0; it < cf.max_iter; ++it) ch[it * chs] = -1;
-  float Jcur = init_tape<TRACK, M>(p, c, x0, S, cf.zpos >= 0 && cf.max_iter > 0);
-  const float Bc0 = barrier_at<M>(p, x0[0], x0[1]);
+  real Jcur = init_tape<TRACK, M>(p, c, x0, S, cf.zpos >= 0 && cf.max_iter > 0);
+  const real Bc0 = barrier_at<M>(p, x0[0], x0[1]);
   bool have_prev = false;
-  float prev = 0.f;
+  real prev = 0.f;
   iters = 0;
   int st = 0;
   int cur = kSlotInit;  // P = 4: the current tape's slot
@@ -1571,7 +1719,7 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
       break;
     }
     pf.mark(ph + 1);
-    float bestJ, al;
+    real bestJ, al;
     int bc;
     Slots Z;
     const int nb = cur < 6 ? 6 : 0;  // first slot of the bank the current tape is not in
@@ -1612,17 +1760,17 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
 }
 
 // ---------------------------------------------------------------------------------------------
-// DDP sensitivity with the paper upper loss + DOC gradient (sens_traj<float, false, false, true>,
+// DDP sensitivity with the paper upper loss + DOC gradient (sens_traj<real, false, false, true>,
 // core/ddp.py:317-427, core/tube_mpc.py:915-976): acc = L, gQ(3), gR(2), gqb
 template <int M, class SV>
 __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV& S, const RA& A8, const RA& A2,
-                                           float* acc) {
+                                           real* acc) {
   const int N = p.N;
-  const float lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
-  const float luu[2] = {2.f * c.R0, 2.f * c.R1};
-  const float pxx[4] = {2.f * c.Qf0, 2.f * c.Qf1, 2.f * c.Qf2, 2.f * c.qb};
-  const float reg = 1e-9f;
-  Riccati<float> R;  // R.Vx holds tilde V_x
+  const real lxx[4] = {2.f * c.Q0, 2.f * c.Q1, 2.f * c.Q2, 2.f * c.qb};
+  const real luu[2] = {2.f * c.R0, 2.f * c.R1};
+  const real pxx[4] = {2.f * c.Qf0, 2.f * c.Qf1, 2.f * c.Qf2, 2.f * c.qb};
+  const real reg = 1e-9f;
+  Riccati<real> R;  // R.Vx holds tilde V_x
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1634,8 +1782,8 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV
     R.Vx[2] = 2.f * (XN.z - RN.z);
     R.Vx[3] = 2.f * XN.w;
   }
-  float gxn, gyn;
-  float dBn;
+  real gxn, gyn;
+  real dBn;
   {
     const f4 XN = S.x(N);
     dBn = dbarrier(p, h_grad<M>(p, XN.x, XN.y, gxn, gyn));
@@ -1652,40 +1800,40 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV
       nR = S.xr(k - 1);
       nV = S.u(k - 1);
     }
-    const float x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w;
-    const float u0 = V.x, u1 = V.y;
-    float sn, cs;
+    const real x0 = X.x, x1 = X.y, x2 = X.z, xb = X.w;
+    const real u0 = V.x, u1 = V.y;
+    real sn, cs;
     vsincos(x2, sn, cs);
-    float gxk, gyk;
-    const float dBk = dbarrier(p, h_grad<M>(p, x0, x1, gxk, gyk));
-    const Jac<float> J = jac(p, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
+    real gxk, gyk;
+    const real dBk = dbarrier(p, h_grad<M>(p, x0, x1, gxk, gyk));
+    const Jac<real> J = jac(p, sn, cs, u0, gxk, gyk, dBk, gxn, gyn, dBn);
     gxn = gxk;
     gyn = gyk;
     dBn = dBk;
-    float Qxx[4][4], Qxu[4][2], Qux[2][4], Quu[2][2];
+    real Qxx[4][4], Qxu[4][2], Qux[2][4], Quu[2][2];
     sens_qblocks(J, R.Vxx, lxx, luu, Qxx, Qxu, Qux, Quu);
-    const float* tv = R.Vx;
-    const float tQu0 = J.b00 * tv[0] + J.b10 * tv[1] + J.b30 * tv[3];
-    const float tQu1 = J.b21 * tv[2] + J.b31 * tv[3];
-    float tQx[4];
+    const real* tv = R.Vx;
+    const real tQu0 = J.b00 * tv[0] + J.b10 * tv[1] + J.b30 * tv[3];
+    const real tQu1 = J.b21 * tv[2] + J.b31 * tv[3];
+    real tQx[4];
     tQx[0] = 2.f * (x0 - Rr.x) + (tv[0] + J.a30 * tv[3]);
     tQx[1] = 2.f * (x1 - Rr.y) + (tv[1] + J.a31 * tv[3]);
     tQx[2] = 2.f * (x2 - Rr.z) + (J.a02 * tv[0] + J.a12 * tv[1] + tv[2] + J.a32 * tv[3]);
     tQx[3] = 2.f * xb + J.g * tv[3];
     const bool act0 = (u0 <= p.umin0 + p.active_tol) || (u0 >= p.umax0 - p.active_tol);
     const bool act1 = (u1 <= p.umin1 + p.active_tol) || (u1 >= p.umax1 - p.active_tol);
-    const float m00 = Quu[0][0] + reg, m11 = Quu[1][1] + reg;
-    const LU2<float> f = lu2(m00, Quu[0][1], Quu[1][0], m11);
-    float Kk[8], kk[2];
+    const real m00 = Quu[0][0] + reg, m11 = Quu[1][1] + reg;
+    const LU2<real> f = lu2(m00, Quu[0][1], Quu[1][0], m11);
+    real Kk[8], kk[2];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float y0, y1;
+      real y0, y1;
       solve_reduced(f, m00, m11, act0, act1, Qux[0][j], Qux[1][j], y0, y1);
       Kk[j] = -y0;
       Kk[4 + j] = -y1;
     }
     {
-      float y0, y1;
+      real y0, y1;
       solve_reduced(f, m00, m11, act0, act1, tQu0, tQu1, y0, y1);
       kk[0] = -y0;
       kk[1] = -y1;
@@ -1698,23 +1846,23 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV
     }
     S.G.store_full(S.r, k, Kk, kk);  // full records in the workspace: its own K and k
     rst4(S.r, A8, k, 0, f4{J.a02, J.a12, J.a30, J.a31});
-    rst4(S.r, A8, k, 16, f4{J.a32, J.b00, J.b10, J.b30});
-    rst2(S.r, A2, k, 0, f2{J.b31, float((act0 ? 1 : 0) + (act1 ? 2 : 0))});
+    rst4(S.r, A8, k, 16 * ES, f4{J.a32, J.b00, J.b10, J.b30});
+    rst2(S.r, A2, k, 0, f2{J.b31, real((act0 ? 1 : 0) + (act1 ? 2 : 0))});
   }
   // forward (:413-425) fused with the upper loss and the DOC gradient
-  float d[4] = {0.f, 0.f, 0.f, 0.f};
-  float L1 = 0.f, L2 = 0.f, gQ0 = 0.f, gQ1 = 0.f, gQ2 = 0.f, gR0 = 0.f, gR1 = 0.f, gqb = 0.f;
-  const float g = p.gamma, dt = p.dt;
+  real d[4] = {0.f, 0.f, 0.f, 0.f};
+  real L1 = 0.f, L2 = 0.f, gQ0 = 0.f, gQ1 = 0.f, gQ2 = 0.f, gR0 = 0.f, gR1 = 0.f, gqb = 0.f;
+  const real g = p.gamma, dt = p.dt;
   struct FwdIn {
     f4 Ka, Kb, A0, A1, X, Rr;
     f2 kf, A2r, V, Q;
   };
   auto fload = [&](FwdIn& F, int k) {
     F.Ka = rld4(S.r, S.G.K, k, 0);
-    F.Kb = rld4(S.r, S.G.K, k, 16);
+    F.Kb = rld4(S.r, S.G.K, k, 16 * ES);
     F.kf = rld2(S.r, S.G.k, k, 0);
     F.A0 = rld4(S.r, A8, k, 0);
-    F.A1 = rld4(S.r, A8, k, 16);
+    F.A1 = rld4(S.r, A8, k, 16 * ES);
     F.A2r = rld2(S.r, A2, k, 0);
     F.X = S.x(k);
     F.Rr = S.xr(k);
@@ -1728,19 +1876,19 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV
     if (k + 1 < N) fload(Fn, k + 1);
     const f4 Ka = F.Ka, Kb = F.Kb, A0 = F.A0, A1 = F.A1;
     const f2 kf = F.kf, A2r = F.A2r;
-    const float a02 = A0.x, a12 = A0.y, a30 = A0.z, a31 = A0.w, a32 = A1.x, b00 = A1.y, b10 = A1.z, b30 = A1.w,
+    const real a02 = A0.x, a12 = A0.y, a30 = A0.z, a31 = A0.w, a32 = A1.x, b00 = A1.y, b10 = A1.z, b30 = A1.w,
                 b31 = A2r.x;
     const int act = (int)A2r.y;
-    const float v0 = (act & 1) ? 0.f : kf.x + (Ka.x * d[0] + Ka.y * d[1] + Ka.z * d[2] + Ka.w * d[3]);
-    const float v1 = (act & 2) ? 0.f : kf.y + (Kb.x * d[0] + Kb.y * d[1] + Kb.z * d[2] + Kb.w * d[3]);
+    const real v0 = (act & 1) ? 0.f : kf.x + (Ka.x * d[0] + Ka.y * d[1] + Ka.z * d[2] + Ka.w * d[3]);
+    const real v1 = (act & 2) ? 0.f : kf.y + (Kb.x * d[0] + Kb.y * d[1] + Kb.z * d[2] + Kb.w * d[3]);
     const f4 X = F.X, Rr = F.Rr;
     const f2 V = F.V, Q = F.Q;
-    const float e0 = X.x - Rr.x;
-    const float e1 = X.y - Rr.y;
-    const float e2 = X.z - Rr.z;
-    const float bb = X.w;
-    const float w0 = V.x - Q.x;
-    const float w1 = V.y - Q.y;
+    const real e0 = X.x - Rr.x;
+    const real e1 = X.y - Rr.y;
+    const real e2 = X.z - Rr.z;
+    const real bb = X.w;
+    const real w0 = V.x - Q.x;
+    const real w1 = V.y - Q.y;
     L1 += e0 * e0 + e1 * e1 + e2 * e2;
     L2 += bb * bb;
     gQ0 += 2.f * e0 * d[0];
@@ -1749,10 +1897,10 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV
     gR0 += 2.f * w0 * v0;
     gR1 += 2.f * w1 * v1;
     gqb += 2.f * bb * d[3];
-    const float n0 = (d[0] + a02 * d[2]) + b00 * v0;
-    const float n1 = (d[1] + a12 * d[2]) + b10 * v0;
-    const float n2 = d[2] + dt * v1;
-    const float n3 = (a30 * d[0] + a31 * d[1] + a32 * d[2] + g * d[3]) + (b30 * v0 + b31 * v1);
+    const real n0 = (d[0] + a02 * d[2]) + b00 * v0;
+    const real n1 = (d[1] + a12 * d[2]) + b10 * v0;
+    const real n2 = d[2] + dt * v1;
+    const real n3 = (a30 * d[0] + a31 * d[1] + a32 * d[2] + g * d[3]) + (b30 * v0 + b31 * v1);
     d[0] = n0;
     d[1] = n1;
     d[2] = n2;
@@ -1762,10 +1910,10 @@ __device__ __forceinline__ int sensitivity(const FP& p, const FCost& c, const SV
 #pragma unroll
   for (int i = 0; i < 4; ++i) ok = ok && finite(d[i]);
   const f4 XN = S.x(N), RN = S.xr(N);
-  const float e0 = XN.x - RN.x;
-  const float e1 = XN.y - RN.y;
-  const float e2 = XN.z - RN.z;
-  const float bb = XN.w;
+  const real e0 = XN.x - RN.x;
+  const real e1 = XN.y - RN.y;
+  const real e2 = XN.z - RN.z;
+  const real bb = XN.w;
   L1 += e0 * e0 + e1 * e1 + e2 * e2;
   L2 += bb * bb;
   acc[0] = L1 + L2;
@@ -1816,7 +1964,7 @@ __device__ __forceinline__ FP pin_p(FP p) {
 #if DTMPC_FAST_PIN
 #pragma unroll
   for (int j = 0; j < Obs<M>::n; ++j) {
-    float vx = p.cx[j], vy = p.cy[j], vr = p.r2[j];
+    real vx = p.cx[j], vy = p.cy[j], vr = p.r2[j];
     __asm__ volatile("" : "+v"(vx));
     __asm__ volatile("" : "+v"(vy));
     __asm__ volatile("" : "+v"(vr));
@@ -1846,7 +1994,7 @@ tube_fast_kernel(FK kk) {
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;  // blockDim: tube_block (64 or 256)
   const int t = gl / P, h = gl % P;  // t: index in the chunk, h: lane of the trajectory
   const int i = i0 + t;              // index in the batch
-  float acc[DTMPC_TUBE_SUMS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  real acc[DTMPC_TUBE_SUMS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   {
     // desynchronise the workgroups' phases: every wave runs the same sequence of passes, so without an
     // offset the whole chip is in the same pass at once -- and the commit (the pass with the most
@@ -1859,19 +2007,19 @@ tube_fast_kernel(FK kk) {
   pf.start();
   if (t < Bc) {
     const size_t nb = (size_t)B;
-    const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
+    const unsigned lo = (unsigned)i * (4u * ES), bb = (unsigned)B * (4u * ES);
     const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
     // record strides: P = 4 keeps kSlots tapes per solve (slot-major inside a row), else one
     constexpr unsigned NS = P == 4 ? kSlots : 1;
-    const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * 8u, l16 = (unsigned)t * 16u, l32 = (unsigned)t * 32u;
-    const SlotMap sm{l16, cb * 16u, l8, cb * 8u};
-    const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * 16u : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * 8u : l8;
+    const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * (8u * ES), l16 = (unsigned)t * (16u * ES), l32 = (unsigned)t * (32u * ES);
+    const SlotMap sm{l16, cb * (16u * ES), l8, cb * (8u * ES)};
+    const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * (16u * ES) : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * (8u * ES) : l8;
     Gains<P> G;
     G.L = (lf4*)lds + (threadIdx.x / P);
     G.w = h == 0;
 
     int st = 0, itn = 0, ita = 0;
-    float x0, x1, x2, xb, y0, y1, y2, yb;
+    real x0, x1, x2, xb, y0, y1, y2, yb;
     {
       KArg* K = kargs();
       x0 = K->a.x[i];
@@ -1887,25 +2035,25 @@ tube_fast_kernel(FK kk) {
     {  // nominal MPC (fixed weights, :813-857)
       KArg* K = kargs();
       Sn.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
-      Sn.XA = RA{K->a.oXn, NS * cb * 16u, x0lo};
-      Sn.UA = RA{K->a.oUn, NS * cb * 8u, u0lo};
+      Sn.XA = RA{K->a.oXn, NS * cb * (16u * ES), x0lo};
+      Sn.UA = RA{K->a.oUn, NS * cb * (8u * ES), u0lo};
       Sn.XRA = Sn.XA;
       Sn.URA = Sn.UA;
       Sn.G = G;
-      Sn.G.K = RA{K->a.oK, cb * 32u, l32};
-      Sn.G.k = RA{K->a.ok, cb * 8u, l8};
+      Sn.G.K = RA{K->a.oK, cb * (32u * ES), l32};
+      Sn.G.k = RA{K->a.ok, cb * (8u * ES), l8};
       Sn.X = Soa<4>{(char*)K->a.Xnom, 4u * bb, L};
       Sn.U = Soa<2>{(char*)K->a.Unom, 2u * bb, L};
       const FP p = phase_p<M>();
       const FCost cn = K->cn;
       const FIlqr cfn = K->cfn;
-      const float xn0[4] = {y0, y1, y2, yb};
+      const real xn0[4] = {y0, y1, y2, yb};
       signed char* ch = K->a.choices ? K->a.choices + i : nullptr;
       st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, sm, itn, pf, ch, nb);
     }
     FCost ca;  // ancillary weights theta (shared by the batch), terminal weight Qa (:885, :891)
     {
-      const float* th = kargs()->a.theta;
+      const real* th = kargs()->a.theta;
       ca.Q0 = ca.Qf0 = th[0];
       ca.Q1 = ca.Qf1 = th[1];
       ca.Q2 = ca.Qf2 = th[2];
@@ -1918,25 +2066,25 @@ tube_fast_kernel(FK kk) {
     {  // ancillary MPC tracking the nominal plan (:863-909)
       KArg* K = kargs();
       Sa.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
-      Sa.XA = RA{K->a.oXa, NS * cb * 16u, x0lo};
-      Sa.UA = RA{K->a.oUa, NS * cb * 8u, u0lo};
+      Sa.XA = RA{K->a.oXa, NS * cb * (16u * ES), x0lo};
+      Sa.UA = RA{K->a.oUa, NS * cb * (8u * ES), u0lo};
       Sa.XRA = Sn.XA;  // the nominal plan as solved (P = 4: its final slot)
       Sa.URA = Sn.UA;
       Sa.G = G;
-      Sa.G.K = RA{K->a.oK, cb * 32u, l32};
-      Sa.G.k = RA{K->a.ok, cb * 8u, l8};
+      Sa.G.K = RA{K->a.oK, cb * (32u * ES), l32};
+      Sa.G.k = RA{K->a.ok, cb * (8u * ES), l8};
       Sa.X = Soa<4>{(char*)K->a.Xaux, 4u * bb, L};
       Sa.U = Soa<2>{(char*)K->a.Uaux, 2u * bb, L};
       const FP p = phase_p<M>();
       const FIlqr cfa = K->cfa;
-      const float xa0[4] = {x0, x1, x2, xb};
+      const real xa0[4] = {x0, x1, x2, xb};
       signed char* ch = K->a.choices ? K->a.choices + (size_t)K->cfn.max_iter * nb + i : nullptr;
       st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, sm, ita, pf, ch, nb);
     }
     pf.mark(8);
     {  // upper loss, DOC sensitivity and gradient (:915-976)
       KArg* K = kargs();
-      const RA A8{K->a.oA8, cb * 32u, l32}, A2{K->a.oA2, cb * 8u, l8};
+      const RA A8{K->a.oA8, cb * (32u * ES), l32}, A2{K->a.oA2, cb * (8u * ES), l8};
       const FP p = phase_p<M>();
       st |= sensitivity<M>(p, ca, Sa, A8, A2, acc);
     }
@@ -1947,9 +2095,9 @@ tube_fast_kernel(FK kk) {
       const FP p = phase_p<M>();
       // the plans' first controls, from the records (the ABI tapes already hold the shifted warm starts)
       const f2 ua = rld2(Sa.r, Sa.UA, 0, 0), un = rld2(Sa.r, Sn.UA, 0, 0);
-      const float u0 = ua.x, u1 = ua.y;
-      const float v0 = un.x, v1 = un.y;
-      float w[3];
+      const real u0 = ua.x, u1 = ua.y;
+      const real v0 = un.x, v1 = un.y;
+      real w[3];
       if (a.disturbance == 0) {
         w[0] = a.w[i];
         w[1] = a.w[nb + i];
@@ -1959,12 +2107,12 @@ tube_fast_kernel(FK kk) {
         philox4x32_10(a.seed, (uint64_t)(a.goff + i), (uint64_t)a.step, r);
 #pragma unroll
         for (int f = 0; f < 3; ++f) {
-          const float u = float(r[f] >> 8) * float(1.0 / 16777216.0);
+          const real u = real(r[f] >> 8) * real(1.0 / 16777216.0);
           w[f] = a.wlo[f] + (a.whi[f] - a.wlo[f]) * u;
         }
       }
       if (a.write_log && h == 0) {
-        float* lg = a.log;
+        real* lg = a.log;
         lg[i] = x0;
         lg[nb + i] = x1;
         lg[2 * nb + i] = x2;
@@ -1980,7 +2128,7 @@ tube_fast_kernel(FK kk) {
         for (int j = 0; j < 7; ++j) lg[(11 + j) * nb + i] = acc[j];
       }
       {
-        float q0 = x0, q1 = x1, q2 = x2, qb = xb, Bc = barrier_at<M>(p, x0, x1);
+        real q0 = x0, q1 = x1, q2 = x2, qb = xb, Bc = barrier_at<M>(p, x0, x1);
         fhat<M>(p, q0, q1, q2, qb, u0, u1, Bc);
         a.x[i] = q0 + w[0];
         a.x[nb + i] = q1 + w[1];
@@ -1988,7 +2136,7 @@ tube_fast_kernel(FK kk) {
         a.b[i] = qb;
       }
       {
-        float q0 = y0, q1 = y1, q2 = y2, qb = yb, Bc = barrier_at<M>(p, y0, y1);
+        real q0 = y0, q1 = y1, q2 = y2, qb = yb, Bc = barrier_at<M>(p, y0, y1);
         fhat<M>(p, q0, q1, q2, qb, v0, v1, Bc);
         a.xbar[i] = q0;
         a.xbar[nb + i] = q1;
@@ -1998,7 +2146,7 @@ tube_fast_kernel(FK kk) {
       acc[7] = 1.f;
       // healthy trajectories only (status 0 and every gradient component within the bound, NaN failing
       // the test); a trajectory's lanes count once
-      float gm = m_abs(acc[1]);
+      real gm = m_abs(acc[1]);
 #pragma unroll
       for (int j = 2; j < 7; ++j) gm = vmaxnan(gm, m_abs(acc[j]));
       if (st || h != 0 || !(gm <= a.gbound)) {
@@ -2017,37 +2165,37 @@ tube_fast_kernel(FK kk) {
   }
   pf.flush();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float ws[DTMPC_TUBE_SUMS];
+  real ws[DTMPC_TUBE_SUMS];
 #pragma unroll
   for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) ws[j] = wave_sum(acc[j]);
   __syncthreads();  // every wave is done with its LDS gains: the first 128 bytes take the wave sums
-  float* red = (float*)lds;
+  real* red = (real*)lds;
   if (lane == 0)
 #pragma unroll
     for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) red[wv * DTMPC_TUBE_SUMS + j] = ws[j];
   __syncthreads();
   if (threadIdx.x < DTMPC_TUBE_SUMS) {
-    float v = 0.f;
+    real v = 0.f;
 #pragma unroll
     for (int q = 0; q < (int)(blockDim.x / 64); ++q) v += red[q * DTMPC_TUBE_SUMS + threadIdx.x];
     kargs()->a.partials[((size_t)blockIdx.x + (size_t)i0 * P / blockDim.x) * DTMPC_TUBE_SUMS + threadIdx.x] = v;
   }
 }
 
-#ifndef DTMPC_FAST_AUX_TU
+#if !defined(DTMPC_FAST_AUX_TU) && !DTMPC_FAST_F64
 // Known-byte calibration launch for the HBM counters (scripts/pmc_calib.py, rocprofv3 --pmc FETCH_SIZE /
 // WRITE_SIZE): the fast kernel's own access pattern -- per-lane 16-byte X records and 8-byte U records
 // [rows][B][W] through one buffer resource, loaded and stored row by row -- copied from src to dst, so
 // the counters' ratio to the known bytes corrects the tube step's figures (MI355X_MICROARCH.md §HBM:
 // "calibrate on a known byte count in your own access pattern").
-__global__ void __launch_bounds__(kBlock) record_stream_kernel(const float* src, float* dst, int B, int N,
+__global__ void __launch_bounds__(kBlock) record_stream_kernel(const real* src, real* dst, int B, int N,
                                                                unsigned bytes) {
   const int t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= B) return;
   const Rsrc rs = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)bytes, 0x00020000);
   const Rsrc rd = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)bytes, 0x00020000);
-  const unsigned cb = (unsigned)B, X = cb * (N + 1) * 16u;
-  const RA XA{0, cb * 16u, (unsigned)t * 16u}, UA{X, cb * 8u, (unsigned)t * 8u};
+  const unsigned cb = (unsigned)B, X = cb * (N + 1) * (16u * ES);
+  const RA XA{0, cb * (16u * ES), (unsigned)t * (16u * ES)}, UA{X, cb * (8u * ES), (unsigned)t * (8u * ES)};
   for (int k = 0; k <= N; ++k) {
     rst4(rd, XA, k, 0, rld4(rs, XA, k, 0));
     if (k < N) rst2(rd, UA, k, 0, rld2(rs, UA, k, 0));
@@ -2065,17 +2213,17 @@ __global__ void __launch_bounds__(kBlock) record_stream_kernel(const float* src,
 // gains K [N][Bc][8] + k [N][Bc][2], the tracking references XR [N+1][Bc][4] / UR [N][Bc][2].
 struct IArgs {
   int B, i0, Bc;
-  const float* x0;
-  const float* Xref;
-  const float* Uref;
-  float* X;
-  float* U;
-  float* K;
-  float* kff;
+  const real* x0;
+  const real* Xref;
+  const real* Uref;
+  real* X;
+  real* U;
+  real* K;
+  real* kff;
   int* iters;
   int* status;
   signed char* choices;
-  float* work;
+  real* work;
   unsigned wsz, oX, oU, oK, ok, oXR, oUR;
 };
 struct IK {
@@ -2104,37 +2252,37 @@ ilqr_fast_kernel(IK kk) {
   const int i = i0 + t;
   if (t >= Bc) return;
   const size_t nb = (size_t)B;
-  const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
+  const unsigned lo = (unsigned)i * (4u * ES), bb = (unsigned)B * (4u * ES);
   const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
   constexpr unsigned NS = P == 4 ? kSlots : 1;
-  const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * 8u, l16 = (unsigned)t * 16u, l32 = (unsigned)t * 32u;
-  const SlotMap sm{l16, cb * 16u, l8, cb * 8u};
-  const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * 16u : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * 8u : l8;
+  const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * (8u * ES), l16 = (unsigned)t * (16u * ES), l32 = (unsigned)t * (32u * ES);
+  const SlotMap sm{l16, cb * (16u * ES), l8, cb * (8u * ES)};
+  const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * (16u * ES) : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * (8u * ES) : l8;
   Solve<TRACK, G0, RG0, P> S;
   S.r = __builtin_amdgcn_make_buffer_rsrc(a.work, 0, (int)a.wsz, 0x00020000);
-  S.XA = RA{a.oX, NS * cb * 16u, x0lo};
-  S.UA = RA{a.oU, NS * cb * 8u, u0lo};
-  S.XRA = RA{a.oXR, cb * 16u, l16};
-  S.URA = RA{a.oUR, cb * 8u, l8};
+  S.XA = RA{a.oX, NS * cb * (16u * ES), x0lo};
+  S.UA = RA{a.oU, NS * cb * (8u * ES), u0lo};
+  S.XRA = RA{a.oXR, cb * (16u * ES), l16};
+  S.URA = RA{a.oUR, cb * (8u * ES), l8};
   S.G.L = (lf4*)lds + (threadIdx.x / P);
   S.G.w = h == 0;
-  S.G.K = RA{a.oK, cb * 32u, l32};
-  S.G.k = RA{a.ok, cb * 8u, l8};
+  S.G.K = RA{a.oK, cb * (32u * ES), l32};
+  S.G.k = RA{a.ok, cb * (8u * ES), l8};
   S.X = Soa<4>{(char*)a.X, 4u * bb, L};
   S.U = Soa<2>{(char*)a.U, 2u * bb, L};
   const FP p = pin_p<M>(ikargs()->p);
   const int N = p.N;
   if (TRACK) {  // the references into records (the lanes of a trajectory split the rows; one wave: in order)
     for (int k = h; k <= N; k += P) {
-      const float* q = a.Xref + (size_t)k * 3 * nb + i;
+      const real* q = a.Xref + (size_t)k * 3 * nb + i;
       rst4(S.r, S.XRA, k, 0, f4{q[0], q[nb], q[2 * nb], 0.f});
       if (k < N) {
-        const float* w = a.Uref + (size_t)k * 2 * nb + i;
+        const real* w = a.Uref + (size_t)k * 2 * nb + i;
         rst2(S.r, S.URA, k, 0, f2{w[0], w[nb]});
       }
     }
   }
-  const float x0[4] = {a.x0[i], a.x0[nb + i], a.x0[2 * nb + i], a.x0[3 * nb + i]};
+  const real x0[4] = {a.x0[i], a.x0[nb + i], a.x0[2 * nb + i], a.x0[3 * nb + i]};
   const FCost c = ikargs()->c;
   const FIlqr cf = ikargs()->cf;
   signed char* ch = a.choices ? a.choices + i : nullptr;
@@ -2147,7 +2295,7 @@ ilqr_fast_kernel(IK kk) {
     f4 Ka, Kb;
     f2 kf;
     S.G.template load<G0>(S.r, k, Ka, Kb, kf);
-    float* Kq = a.K + (size_t)k * 8 * nb + i;
+    real* Kq = a.K + (size_t)k * 8 * nb + i;
     Kq[0] = Ka.x;
     Kq[nb] = Ka.y;
     Kq[2 * nb] = Ka.z;
@@ -2156,7 +2304,7 @@ ilqr_fast_kernel(IK kk) {
     Kq[5 * nb] = Kb.y;
     Kq[6 * nb] = Kb.z;
     Kq[7 * nb] = Kb.w;
-    float* kq = a.kff + (size_t)k * 2 * nb + i;
+    real* kq = a.kff + (size_t)k * 2 * nb + i;
     kq[0] = kf.x;
     kq[nb] = kf.y;
   }
@@ -2174,19 +2322,19 @@ ilqr_fast_kernel(IK kk) {
 // each trajectory's solve status to `sst`; dtmpc_general_step's sensitivity / IFT kernel follows.
 struct GSArgs {
   int B, i0, Bc;
-  const float* theta;  // [2][12] raw: row 0 ancillary theta, row 1 nominal theta-bar
+  const real* theta;  // [2][12] raw: row 0 ancillary theta, row 1 nominal theta-bar
   f4 tgt;
-  const float* x;
-  const float* b;
-  const float* xbar;
-  const float* bbar;
-  float* Xnom;
-  float* Unom;
-  float* Xaux;
-  float* Uaux;
+  const real* x;
+  const real* b;
+  const real* xbar;
+  const real* bbar;
+  real* Xnom;
+  real* Unom;
+  real* Xaux;
+  real* Uaux;
   int* iters;
   int* sst;
-  float* work;
+  real* work;
   unsigned wsz, oXn, oUn, oXa, oUa, oK, ok;
 };
 struct GSK {
@@ -2203,7 +2351,7 @@ __device__ __forceinline__ const GSK* gskargs() {
 
 // the DBaS constants of a parameterised solve, formed in f32 on the device as the generic kernels form
 // them (barrier_relaxed: a = max(alpha, eps), 1 / a and 1 / a^2 correctly rounded)
-__device__ __forceinline__ FP general_fp(FP p, const GPar<float>& g) {
+__device__ __forceinline__ FP general_fp(FP p, const GPar<real>& g) {
   DTMPC_NOCONTRACT
   p.gamma = g.gamma;
   p.tight = g.tight;
@@ -2220,7 +2368,7 @@ __device__ __forceinline__ FP general_fp(FP p, const GPar<float>& g) {
 // theta on the device, so the kernel branches -- uniformly -- between the two instantiations).  XA / UA
 // come back as the solved tape's records (P = 4: its final slot).
 template <bool TRACK, int M, int P, int NCV, bool G0>
-__device__ __forceinline__ int general_solve(const FP& p, const FCost& c, const FIlqr& cf, const float* x0, Rsrc r,
+__device__ __forceinline__ int general_solve(const FP& p, const FCost& c, const FIlqr& cf, const real* x0, Rsrc r,
                                              RA& XA, RA& UA, const RA& XRA, const RA& URA, const Gains<P>& G,
                                              const Soa<4>& X, const Soa<2>& U, int h, const SlotMap& sm, int& it,
                                              Prof& pf) {
@@ -2251,28 +2399,28 @@ general_solve_fast_kernel(GSK kk) {
   const int i = i0 + t;
   if (t >= Bc) return;
   const size_t nb = (size_t)B;
-  const unsigned lo = (unsigned)i * 4u, bb = (unsigned)B * 4u;
+  const unsigned lo = (unsigned)i * (4u * ES), bb = (unsigned)B * (4u * ES);
   const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
   constexpr unsigned NS = P == 4 ? kSlots : 1;
-  const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * 8u, l16 = (unsigned)t * 16u, l32 = (unsigned)t * 32u;
-  const SlotMap sm{l16, cb * 16u, l8, cb * 8u};
-  const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * 16u : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * 8u : l8;
+  const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * (8u * ES), l16 = (unsigned)t * (16u * ES), l32 = (unsigned)t * (32u * ES);
+  const SlotMap sm{l16, cb * (16u * ES), l8, cb * (8u * ES)};
+  const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * (16u * ES) : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * (8u * ES) : l8;
   Gains<P> G;
   G.L = (lf4*)lds + (threadIdx.x / P);
   G.w = h == 0;
-  G.K = RA{a.oK, cb * 32u, l32};
-  G.k = RA{a.ok, cb * 8u, l8};
+  G.K = RA{a.oK, cb * (32u * ES), l32};
+  G.k = RA{a.ok, cb * (8u * ES), l8};
   const Rsrc r = __builtin_amdgcn_make_buffer_rsrc(a.work, 0, (int)a.wsz, 0x00020000);
   int st = 0, itn = 0, ita = 0;
   Prof pf;
   pf.start();
-  RA XN{a.oXn, NS * cb * 16u, x0lo}, UN{a.oUn, NS * cb * 8u, u0lo};
+  RA XN{a.oXn, NS * cb * (16u * ES), x0lo}, UN{a.oUn, NS * cb * (8u * ES), u0lo};
   {  // nominal MPC with theta-bar (:217-291)
-    const GPar<float> pn = gpar_from<float>(a.theta + DTMPC_P_COUNT, true);
+    const GPar<real> pn = gpar_from<real>(a.theta + DTMPC_P_COUNT, true);
     const FP p = pin_p<M | kTight>(general_fp(gskargs()->p, pn));
     const FCost cn{pn.Q[0], pn.Q[1], pn.Q[2], pn.R[0], pn.R[1], pn.Qf[0], pn.Qf[1], pn.Qf[2], pn.qb, a.tgt};
     const FIlqr cfn = gskargs()->cfn;
-    const float xn0[4] = {a.xbar[i], a.xbar[nb + i], a.xbar[2 * nb + i], a.bbar[i]};
+    const real xn0[4] = {a.xbar[i], a.xbar[nb + i], a.xbar[2 * nb + i], a.bbar[i]};
     const Soa<4> X{(char*)a.Xnom, 4u * bb, L};
     const Soa<2> U{(char*)a.Unom, 2u * bb, L};
     if (pn.gamma == 0.f)
@@ -2281,13 +2429,13 @@ general_solve_fast_kernel(GSK kk) {
       st |= general_solve<false, M | kTight, P, NCV, false>(p, cn, cfn, xn0, r, XN, UN, XN, UN, G, X, U, h, sm, itn, pf);
   }
   {  // ancillary MPC with theta tracking the nominal plan as solved (:296-392)
-    RA XA{a.oXa, NS * cb * 16u, x0lo}, UA{a.oUa, NS * cb * 8u, u0lo};
-    const GPar<float> pa = gpar_from<float>(a.theta, false);
+    RA XA{a.oXa, NS * cb * (16u * ES), x0lo}, UA{a.oUa, NS * cb * (8u * ES), u0lo};
+    const GPar<real> pa = gpar_from<real>(a.theta, false);
     const FP p = pin_p<M>(general_fp(gskargs()->p, pa));
     const FCost ca{pa.Q[0], pa.Q[1], pa.Q[2], pa.R[0], pa.R[1], pa.Qf[0], pa.Qf[1], pa.Qf[2], pa.qb,
                    f4{0.f, 0.f, 0.f, 0.f}};
     const FIlqr cfa = gskargs()->cfa;
-    const float xa0[4] = {a.x[i], a.x[nb + i], a.x[2 * nb + i], a.b[i]};
+    const real xa0[4] = {a.x[i], a.x[nb + i], a.x[2 * nb + i], a.b[i]};
     const Soa<4> X{(char*)a.Xaux, 4u * bb, L};
     const Soa<2> U{(char*)a.Uaux, 2u * bb, L};
     if (pa.gamma == 0.f)
@@ -2305,32 +2453,35 @@ general_solve_fast_kernel(GSK kk) {
 }
 
 
-}  // namespace fk
+}  // namespace FK_NS
 
 // ---------------------------------------------------------------------------------------------
 // host side
+using FK_NS::ES;
+using FK_NS::real;
+constexpr int kFastDtype = DTMPC_FAST_F64 ? DTMPC_F64 : DTMPC_F32;  // the precision this unit instantiates
 
 static bool fast_spec_ok(const dtmpc_spec* sp) {
   return sp->obs_aggregation == DTMPC_OBS_SMOOTHMIN && sp->n_obstacles >= 1 && sp->n_obstacles <= 8 &&
          sp->barrier_type == DTMPC_BARRIER_INVERSE && sp->h_offset == 0.0;
 }
 
-static fk::FIlqr fast_ilqr(const dtmpc_ilqr_cfg& c) {
-  const DIlqr<float> d = make_ilqr<float>(c);
-  fk::FIlqr o;
+static FK_NS::FIlqr fast_ilqr(const dtmpc_ilqr_cfg& c) {
+  const DIlqr<real> d = make_ilqr<real>(c);
+  FK_NS::FIlqr o;
   o.max_iter = d.max_iter;
   o.zpos = d.zpos;
   o.tol = d.tol;
   o.reg = d.reg;
-  for (int q = 0; q < fk::NC; ++q) {
+  for (int q = 0; q < FK_NS::NC; ++q) {
     o.cal[q] = d.calphas[q];
     o.cpos[q] = d.cpos[q];
   }
   return o;
 }
 
-static void fast_p(const dtmpc_spec* sp, fk::FP& p) {
-  const DSpec<float> s = make_spec<float>(*sp);
+static void fast_p(const dtmpc_spec* sp, FK_NS::FP& p) {
+  const DSpec<real> s = make_spec<real>(*sp);
   p.N = s.N;
   p.dt = s.dt;
   p.umin0 = s.umin0;
@@ -2347,7 +2498,7 @@ static void fast_p(const dtmpc_spec* sp, fk::FP& p) {
   p.a = s.alpha > s.eps ? s.alpha : s.eps;
   p.a2 = p.a * p.a;
   p.a3 = p.a2 * p.a;
-  volatile float one = 1.0f;  // f32 division on the host: correctly rounded, as the device's
+  volatile real one = 1.0f;  // f32 division on the host: correctly rounded, as the device's
   p.inv_a = one / p.a;
   p.inv_a2 = one / p.a2;
   for (int i = 0; i < 8; ++i) {
@@ -2371,13 +2522,13 @@ struct FastLayout {
   unsigned oXn, oXa, oUn, oUa, oK, ok, oA8, oA2, wsz;
 };
 static int64_t fast_bytes_per_traj(int N, int lanes) {
-  const int64_t ns = lanes == 4 ? fk::kSlots : 1;
-  return ns * ((int64_t)(N + 1) * 32 + (int64_t)N * 16) + (int64_t)N * 80;
+  const int64_t ns = lanes == 4 ? FK_NS::kSlots : 1;
+  return ns * ((int64_t)(N + 1) * 32 * ES + (int64_t)N * 16 * ES) + (int64_t)N * 80 * ES;
 }
 static FastLayout fast_layout(int N, int64_t Bc, int lanes) {
-  const int64_t ns = lanes == 4 ? fk::kSlots : 1;
-  const unsigned X = (unsigned)(ns * Bc * (N + 1) * 16), U = (unsigned)(ns * Bc * N * 8);
-  const unsigned K = (unsigned)(Bc * N * 32), k = (unsigned)(Bc * N * 8);
+  const int64_t ns = lanes == 4 ? FK_NS::kSlots : 1;
+  const unsigned X = (unsigned)(ns * Bc * (N + 1) * 16 * ES), U = (unsigned)(ns * Bc * N * 8 * ES);
+  const unsigned K = (unsigned)(Bc * N * 32 * ES), k = (unsigned)(Bc * N * 8 * ES);
   FastLayout f;
   f.oXn = 0;
   f.oXa = X;
@@ -2390,64 +2541,65 @@ static FastLayout fast_layout(int N, int64_t Bc, int lanes) {
   f.wsz = f.oA2 + k;
   return f;
 }
-int64_t tube_fast_chunk_max(int N, int lanes) {
+int64_t FKN(tube_fast_chunk_max)(int N, int lanes) {
   const int64_t c = ((int64_t)0x7fffffff / fast_bytes_per_traj(N, lanes)) / kBlock * kBlock;
   return c < kBlock ? kBlock : c;
 }
-size_t tube_fast_workspace_bytes(int N, int64_t B, int lanes, int64_t chunk) {
+size_t FKN(tube_fast_workspace_bytes)(int N, int64_t B, int lanes, int64_t chunk) {
   const int64_t b = B < chunk ? B : chunk;
   return (size_t)b * (size_t)fast_bytes_per_traj(N, lanes);
 }
 
-bool tube_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf) {
-  const char* e = getenv("DTMPC_FAST");
+bool FKN(tube_fast_eligible)(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf) {
+  const char* e = getenv(DTMPC_FAST_F64 ? "DTMPC_FAST64" : "DTMPC_FAST");  // "0": the generic kernel (A/B, tests)
   if (e && e[0] == '0' && e[1] == 0) return false;
-  if (dtype != DTMPC_F32 || !fast_spec_ok(sp)) return false;
+  if (DTMPC_FAST_F64 && (e = getenv("DTMPC_FAST")) && e[0] == '0' && e[1] == 0) return false;
+  if (dtype != kFastDtype || !fast_spec_ok(sp)) return false;
   if (cf->nominal.kind != DTMPC_COST_TARGET || cf->nominal.wrap_angle) return false;
-  const DIlqr<float> n = make_ilqr<float>(cf->nom_ilqr), a = make_ilqr<float>(cf->aux_ilqr);
-  return n.nc == fk::NC && a.nc == fk::NC;
+  const DIlqr<real> n = make_ilqr<real>(cf->nom_ilqr), a = make_ilqr<real>(cf->aux_ilqr);
+  return n.nc == FK_NS::NC && a.nc == FK_NS::NC;
 }
 
-int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
+int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
                      const dtmpc_tube_state* S, const void* w, hipStream_t st) {
-  fk::FK kk;
+  FK_NS::FK kk;
   std::memset(&kk, 0, sizeof(kk));
   fast_p(sp, kk.p);
-  const DCost<float> c = make_cost<float>(cf->nominal);
-  kk.cn = fk::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb, fk::f4{c.t0, c.t1, c.t2, 0.f}};
+  const DCost<real> c = make_cost<real>(cf->nominal);
+  kk.cn = FK_NS::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb, FK_NS::f4{c.t0, c.t1, c.t2, 0.f}};
   kk.cfn = fast_ilqr(cf->nom_ilqr);
   kk.cfa = fast_ilqr(cf->aux_ilqr);
-  fk::FArgs& a = kk.a;
+  FK_NS::FArgs& a = kk.a;
   const int N = sp->horizon;
   a.B = (int)B;
   a.goff = goff;
   a.step = step;
-  a.x = (float*)S->x;
-  a.b = (float*)S->b;
-  a.xbar = (float*)S->xbar;
-  a.bbar = (float*)S->bbar;
-  a.Xnom = (float*)S->Xnom;
-  a.Unom = (float*)S->Unom;
-  a.Xaux = (float*)S->Xaux;
-  a.Uaux = (float*)S->Uaux;
-  a.work = (float*)S->work;
-  a.theta = (const float*)S->theta;
-  a.partials = (float*)S->partials;
-  a.log = (float*)S->log;
+  a.x = (real*)S->x;
+  a.b = (real*)S->b;
+  a.xbar = (real*)S->xbar;
+  a.bbar = (real*)S->bbar;
+  a.Xnom = (real*)S->Xnom;
+  a.Unom = (real*)S->Unom;
+  a.Xaux = (real*)S->Xaux;
+  a.Uaux = (real*)S->Uaux;
+  a.work = (real*)S->work;
+  a.theta = (const real*)S->theta;
+  a.partials = (real*)S->partials;
+  a.log = (real*)S->log;
   a.status = S->status;
   a.iters = S->iters;
-  a.w = (const float*)w;
+  a.w = (const real*)w;
   a.choices = (signed char*)S->choices;
-  a.gbound = cf->grad_bound > 0 ? float(cf->grad_bound) : __builtin_inff();
+  a.gbound = cf->grad_bound > 0 ? real(cf->grad_bound) : real(__builtin_inf());
   a.disturbance = cf->disturbance;
   a.write_log = (cf->write_log && S->log) ? 1 : 0;
   a.seed = cf->seed;
   for (int f = 0; f < 3; ++f) {
-    a.wlo[f] = float(cf->w_low[f]);
-    a.whi[f] = float(cf->w_high[f]);
+    a.wlo[f] = real(cf->w_low[f]);
+    a.whi[f] = real(cf->w_high[f]);
   }
   const int lanes = S->lanes;
-  // gamma = 0 (the paper's DBaS): the compact gain records (fk::Gains) and the Riccati step without the
+  // gamma = 0 (the paper's DBaS): the compact gain records (FK_NS::Gains) and the Riccati step without the
   // barrier state's zero column (riccati_pk<true>).  DTMPC_FAST_G0 (environment, read at each call) = 0
   // keeps the general records and recursion, = 1 the compact records with the general recursion: the
   // tests compare 1 with 0 for exact equality (records) and the default with the oracle builds.
@@ -2461,7 +2613,8 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
   // the batch in chunks whose workspace records fit one buffer resource (< 2^31 bytes), each chunk a
   // multiple of the workgroup size (its partial-sum rows follow the previous chunk's); the chunk comes
   // from the state (dtmpc_tube_chunk, validated against the workspace by dtmpc_tube_step)
-  const int64_t chunk = S->chunk;
+  // (f64 records are twice as large: its chunk is at most half the f32 one, dtmpc_tube_workspace_bytes)
+  const int64_t cmax = FKN(tube_fast_chunk_max)(N, lanes), chunk = S->chunk < cmax ? S->chunk : cmax;
   for (int64_t c0 = 0; c0 < B; c0 += chunk) {
     const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
     a.i0 = (int)c0;
@@ -2478,7 +2631,7 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
     a.wsz = f.wsz;
     const int bs = tube_block(B, lanes);  // 64 while the batch leaves SIMDs idle: one wave per workgroup
     const dim3 grid = dim3((unsigned)((Bc * lanes + bs - 1) / bs));
-#define FAST_LAUNCH(m, l, g) hipLaunchKernelGGL((fk::tube_fast_kernel<m, l, g>), grid, dim3(bs), 0, st, kk)
+#define FAST_LAUNCH(m, l, g) hipLaunchKernelGGL((FK_NS::tube_fast_kernel<m, l, g>), grid, dim3(bs), 0, st, kk)
 #define FAST_LANES(m, l) \
   if (g0 == 2) FAST_LAUNCH(m, l, 2); else if (g0) FAST_LAUNCH(m, l, 1); else FAST_LAUNCH(m, l, 0);
 #ifdef DTMPC_FAST_ISA_ONLY  // ISA inspection builds: one instantiation (lanes 1, gamma = 0 records + Riccati)
@@ -2516,71 +2669,71 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
 
 // the standalone solve's records per trajectory: X / U slots, gains K + k, tracking references
 static int64_t ilqr_fast_bytes_per_traj(int N, int lanes) {
-  const int64_t ns = lanes == 4 ? fk::kSlots : 1;
-  return ns * ((int64_t)(N + 1) * 16 + (int64_t)N * 8) + (int64_t)N * 40 + (int64_t)(N + 1) * 16 + (int64_t)N * 8;
+  const int64_t ns = lanes == 4 ? FK_NS::kSlots : 1;
+  return ns * ((int64_t)(N + 1) * 16 * ES + (int64_t)N * 8 * ES) + (int64_t)N * 40 * ES + (int64_t)(N + 1) * 16 * ES + (int64_t)N * 8 * ES;
 }
-int64_t ilqr_fast_chunk_max(int N, int lanes) {
+int64_t FKN(ilqr_fast_chunk_max)(int N, int lanes) {
   const int64_t c = ((int64_t)0x7fffffff / ilqr_fast_bytes_per_traj(N, lanes)) / kBlock * kBlock;
   return c < kBlock ? kBlock : c;
 }
-size_t ilqr_fast_workspace_bytes(int N, int64_t B, int lanes) {
-  const int64_t ch = ilqr_fast_chunk_max(N, lanes), b = B < ch ? B : ch;
+size_t FKN(ilqr_fast_workspace_bytes)(int N, int64_t B, int lanes) {
+  const int64_t ch = FKN(ilqr_fast_chunk_max)(N, lanes), b = B < ch ? B : ch;
   return (size_t)b * (size_t)ilqr_fast_bytes_per_traj(N, lanes);
 }
 
-bool ilqr_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf) {
+bool FKN(ilqr_fast_eligible)(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf) {
   const char* e = getenv("DTMPC_FAST");
   if (e && e[0] == '0' && e[1] == 0) return false;
-  if (dtype != DTMPC_F32 || !fast_spec_ok(sp) || c->wrap_angle) return false;
-  return make_ilqr<float>(*cf).nc == fk::NC;
+  if (dtype != kFastDtype || !fast_spec_ok(sp) || c->wrap_angle) return false;
+  return make_ilqr<real>(*cf).nc == FK_NS::NC;
 }
 
-int launch_ilqr_fast(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, const void* x0,
+int FKN(launch_ilqr_fast)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, const void* x0,
                      const void* Xref, const void* Uref, void* X, void* U, void* K, void* kff, int* iters, int* status,
                      signed char* choices, int lanes, void* work, size_t work_bytes, hipStream_t st) {
   const int N = sp->horizon;
   if (lanes != 1 && lanes != 2 && lanes != 4) return set_err(DTMPC_ERR_BAD_ARG, "lanes must be 1, 2 or 4");
-  if (!work || work_bytes < ilqr_fast_workspace_bytes(N, B, lanes))
+  if (!work || work_bytes < FKN(ilqr_fast_workspace_bytes)(N, B, lanes))
     return set_err(DTMPC_ERR_BAD_ARG, "work_bytes < dtmpc_ilqr_workspace_bytes(...)");
-  fk::IK kk;
+  FK_NS::IK kk;
   std::memset(&kk, 0, sizeof(kk));
   fast_p(sp, kk.p);
-  const DCost<float> c = make_cost<float>(*cp);
+  const DCost<real> c = make_cost<real>(*cp);
   const bool track = cp->kind == DTMPC_COST_TRACK;
-  kk.c = fk::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb,
-                   track ? fk::f4{0.f, 0.f, 0.f, 0.f} : fk::f4{c.t0, c.t1, c.t2, 0.f}};
+  kk.c = FK_NS::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb,
+                   track ? FK_NS::f4{0.f, 0.f, 0.f, 0.f} : FK_NS::f4{c.t0, c.t1, c.t2, 0.f}};
   kk.cf = fast_ilqr(*cf);
-  fk::IArgs& a = kk.a;
+  FK_NS::IArgs& a = kk.a;
   a.B = (int)B;
-  a.x0 = (const float*)x0;
-  a.Xref = (const float*)Xref;
-  a.Uref = (const float*)Uref;
-  a.X = (float*)X;
-  a.U = (float*)U;
-  a.K = (float*)K;
-  a.kff = (float*)kff;
+  a.x0 = (const real*)x0;
+  a.Xref = (const real*)Xref;
+  a.Uref = (const real*)Uref;
+  a.X = (real*)X;
+  a.U = (real*)U;
+  a.K = (real*)K;
+  a.kff = (real*)kff;
   a.iters = iters;
   a.status = status;
   a.choices = choices;
-  a.work = (float*)work;
+  a.work = (real*)work;
   // gamma = 0: the compact gain records and the Riccati step without the barrier state's column
   const int g0 = kk.p.gamma == 0.f ? 2 : 0;
-  const int64_t chunk = ilqr_fast_chunk_max(N, lanes);
+  const int64_t chunk = FKN(ilqr_fast_chunk_max)(N, lanes);
   for (int64_t c0 = 0; c0 < B; c0 += chunk) {
     const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
-    const int64_t ns = lanes == 4 ? fk::kSlots : 1;
+    const int64_t ns = lanes == 4 ? FK_NS::kSlots : 1;
     a.i0 = (int)c0;
     a.Bc = (int)Bc;
     a.oX = 0;
-    a.oU = (unsigned)(ns * Bc * (N + 1) * 16);
-    a.oK = a.oU + (unsigned)(ns * Bc * N * 8);
-    a.ok = a.oK + (unsigned)(Bc * N * 32);
-    a.oXR = a.ok + (unsigned)(Bc * N * 8);
-    a.oUR = a.oXR + (unsigned)(Bc * (N + 1) * 16);
-    a.wsz = a.oUR + (unsigned)(Bc * N * 8);
+    a.oU = (unsigned)(ns * Bc * (N + 1) * 16 * ES);
+    a.oK = a.oU + (unsigned)(ns * Bc * N * 8 * ES);
+    a.ok = a.oK + (unsigned)(Bc * N * 32 * ES);
+    a.oXR = a.ok + (unsigned)(Bc * N * 8 * ES);
+    a.oUR = a.oXR + (unsigned)(Bc * (N + 1) * 16 * ES);
+    a.wsz = a.oUR + (unsigned)(Bc * N * 8 * ES);
     const int bs = tube_block(B, lanes);
     const dim3 grid = dim3((unsigned)((Bc * lanes + bs - 1) / bs));
-#define IL_LAUNCH(m, l, t, g) hipLaunchKernelGGL((fk::ilqr_fast_kernel<m, l, t, g>), grid, dim3(bs), 0, st, kk)
+#define IL_LAUNCH(m, l, t, g) hipLaunchKernelGGL((FK_NS::ilqr_fast_kernel<m, l, t, g>), grid, dim3(bs), 0, st, kk)
 #define IL_G(m, l, t) \
   if (g0 == 2) IL_LAUNCH(m, l, t, 2); else IL_LAUNCH(m, l, t, 0);
 #define IL_T(m, l) \
@@ -2611,67 +2764,67 @@ int launch_ilqr_fast(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilq
 // one lane per trajectory: the records of both solves (two tapes of (N+1) x 16 + N x 8 bytes and the
 // gains' N x 40) fit in the generic scratch of dtmpc_general_workspace_bytes (N x 80 + (N+1) x 40)
 static int64_t general_fast_bytes_per_traj(int N) {
-  return 2 * ((int64_t)(N + 1) * 16 + (int64_t)N * 8) + (int64_t)N * 40;
+  return 2 * ((int64_t)(N + 1) * 16 * ES + (int64_t)N * 8 * ES) + (int64_t)N * 40 * ES;
 }
 
-bool general_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_general_cfg* cf) {
+bool FKN(general_fast_eligible)(int dtype, const dtmpc_spec* sp, const dtmpc_general_cfg* cf) {
   const char* e = getenv("DTMPC_FAST");
   if (e && e[0] == '0' && e[1] == 0) return false;
   // the tightening s comes from theta-bar (spec.h_offset is not used by the general path)
-  if (dtype != DTMPC_F32 || sp->obs_aggregation != DTMPC_OBS_SMOOTHMIN || sp->n_obstacles < 1 ||
+  if (dtype != kFastDtype || sp->obs_aggregation != DTMPC_OBS_SMOOTHMIN || sp->n_obstacles < 1 ||
       sp->n_obstacles > 8 || sp->barrier_type != DTMPC_BARRIER_INVERSE)
     return false;
   // six rolled-out candidates (the paper's seven alphas) or four (ILQRConfig's default alphas), the
   // same list in both solves (check_general)
-  const int nc = make_ilqr<float>(cf->nom_ilqr).nc;
-  return (nc == fk::NC || nc == 4) && make_ilqr<float>(cf->aux_ilqr).nc == nc;
+  const int nc = make_ilqr<real>(cf->nom_ilqr).nc;
+  return (nc == FK_NS::NC || nc == 4) && make_ilqr<real>(cf->aux_ilqr).nc == nc;
 }
 
-int launch_general_solve_fast(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int64_t B,
+int FKN(launch_general_solve_fast)(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int64_t B,
                               const dtmpc_general_state* S, int* sst, hipStream_t st) {
   const int N = sp->horizon;
-  fk::GSK kk;
+  FK_NS::GSK kk;
   std::memset(&kk, 0, sizeof(kk));
   fast_p(sp, kk.p);
   kk.cfn = fast_ilqr(cf->nom_ilqr);
   kk.cfa = fast_ilqr(cf->aux_ilqr);
-  fk::GSArgs& a = kk.a;
+  FK_NS::GSArgs& a = kk.a;
   a.B = (int)B;
-  a.theta = (const float*)S->theta;
-  a.tgt = fk::f4{float(cf->target[0]), float(cf->target[1]), float(cf->target[2]), 0.f};
-  a.x = (const float*)S->x;
-  a.b = (const float*)S->b;
-  a.xbar = (const float*)S->xbar;
-  a.bbar = (const float*)S->bbar;
-  a.Xnom = (float*)S->Xnom;
-  a.Unom = (float*)S->Unom;
-  a.Xaux = (float*)S->Xaux;
-  a.Uaux = (float*)S->Uaux;
+  a.theta = (const real*)S->theta;
+  a.tgt = FK_NS::f4{real(cf->target[0]), real(cf->target[1]), real(cf->target[2]), 0.f};
+  a.x = (const real*)S->x;
+  a.b = (const real*)S->b;
+  a.xbar = (const real*)S->xbar;
+  a.bbar = (const real*)S->bbar;
+  a.Xnom = (real*)S->Xnom;
+  a.Unom = (real*)S->Unom;
+  a.Xaux = (real*)S->Xaux;
+  a.Uaux = (real*)S->Uaux;
   a.iters = S->iters;
   a.sst = sst;
-  a.work = (float*)S->work;
-  const int nc = make_ilqr<float>(cf->nom_ilqr).nc;
+  a.work = (real*)S->work;
+  const int nc = make_ilqr<real>(cf->nom_ilqr).nc;
   const int bs = tube_block(B, 1);
   const int64_t chunk = ((int64_t)0x7fffffff / general_fast_bytes_per_traj(N)) / kBlock * kBlock;
   for (int64_t c0 = 0; c0 < B; c0 += chunk) {
     const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
     a.i0 = (int)c0;
     a.Bc = (int)Bc;
-    const unsigned X = (unsigned)(Bc * (N + 1) * 16), U = (unsigned)(Bc * N * 8);
+    const unsigned X = (unsigned)(Bc * (N + 1) * 16 * ES), U = (unsigned)(Bc * N * 8 * ES);
     a.oXn = 0;
     a.oXa = X;
     a.oUn = 2 * X;
     a.oUa = 2 * X + U;
     a.oK = 2 * X + 2 * U;
-    a.ok = a.oK + (unsigned)(Bc * N * 32);
-    a.wsz = a.ok + (unsigned)(Bc * N * 8);
+    a.ok = a.oK + (unsigned)(Bc * N * 32 * ES);
+    a.wsz = a.ok + (unsigned)(Bc * N * 8 * ES);
 #define GS_LAUNCH(m, n)                                                                                   \
-  hipLaunchKernelGGL((fk::general_solve_fast_kernel<m, 1, n>), dim3((unsigned)((Bc + bs - 1) / bs)), dim3(bs), 0, \
+  hipLaunchKernelGGL((FK_NS::general_solve_fast_kernel<m, 1, n>), dim3((unsigned)((Bc + bs - 1) / bs)), dim3(bs), 0, \
                      st, kk)
 #define GS_CASE(m)                 \
   case m:                          \
     if (nc == 4) GS_LAUNCH(m, 4);  \
-    else GS_LAUNCH(m, fk::NC);     \
+    else GS_LAUNCH(m, FK_NS::NC);     \
     break;
     switch (sp->n_obstacles) {
 #if defined(DTMPC_FAST_M_ONLY)
@@ -2693,14 +2846,14 @@ int launch_general_solve_fast(const dtmpc_spec* sp, const dtmpc_general_cfg* cf,
 
 }  // namespace dtmpc
 
-#ifndef DTMPC_FAST_AUX_TU
+#if !defined(DTMPC_FAST_AUX_TU) && !DTMPC_FAST_F64
 extern "C" {
 // diagnostics (not part of include/dtmpc.h): the counter-calibration copy of record_stream_kernel over
 // src / dst buffers of (N+1) x 16 + N x 8 bytes per trajectory (< 2^31 bytes)
 int dtmpc_diag_record_stream(int64_t B, int32_t N, const void* src, void* dst, void* stream) {
   const int64_t bytes = B * ((int64_t)(N + 1) * 16 + (int64_t)N * 8);
   if (B < 1 || N < 1 || bytes >= 0x7fffffff || !src || !dst) return dtmpc::set_err(DTMPC_ERR_BAD_ARG, "bad sizes");
-  hipLaunchKernelGGL(dtmpc::fk::record_stream_kernel, dtmpc::grid_for(B), dim3(dtmpc::kBlock), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(dtmpc::FK_NS::record_stream_kernel, dtmpc::grid_for(B), dim3(dtmpc::kBlock), 0, (hipStream_t)stream,
                      (const float*)src, (float*)dst, (int)B, (int)N, (unsigned)bytes);
   return dtmpc::check_launch("record_stream_kernel");
 }
@@ -2714,11 +2867,11 @@ int dtmpc_prof_read_fast(void* host16) {
 }
 int dtmpc_prof_reset_fast(void) {
   unsigned long long z[64] = {0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(dtmpc::fk::g_lsstat), z, sizeof(z)) != hipSuccess) return 1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(dtmpc::FK_NS::g_lsstat), z, sizeof(z)) != hipSuccess) return 1;
   return hipMemcpyToSymbol(HIP_SYMBOL(dtmpc::g_prof), z, 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
 }
 int dtmpc_prof_lsstat_fast(void* host64) {
-  return hipMemcpyFromSymbol(host64, HIP_SYMBOL(dtmpc::fk::g_lsstat), 64 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+  return hipMemcpyFromSymbol(host64, HIP_SYMBOL(dtmpc::FK_NS::g_lsstat), 64 * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
 }
 }
 #endif

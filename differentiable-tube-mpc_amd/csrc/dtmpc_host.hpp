@@ -183,6 +183,13 @@ int64_t tube_fast_chunk_max(int N, int lanes);
 size_t tube_fast_workspace_bytes(int N, int64_t B, int lanes, int64_t chunk);
 int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
                      const dtmpc_tube_state* S, const void* w, hipStream_t st);
+// the same tube step in f64 (dtmpc_fast64.hip: dtmpc_fast.hip with real = double); its chunk is clamped to
+// tube_fast_chunk_max64 at launch
+bool tube_fast_eligible64(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf);
+int64_t tube_fast_chunk_max64(int N, int lanes);
+size_t tube_fast_workspace_bytes64(int N, int64_t B, int lanes, int64_t chunk);
+int launch_tube_fast64(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
+                       const dtmpc_tube_state* S, const void* w, hipStream_t st);
 // the standalone batched iLQR on the same configuration (dtmpc_ilqr_solve_ws)
 bool ilqr_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf);
 size_t ilqr_fast_workspace_bytes(int N, int64_t B, int lanes);

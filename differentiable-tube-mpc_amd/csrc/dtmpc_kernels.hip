@@ -751,7 +751,13 @@ size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t
   // generic kernel: sensitivity K / kf / AB (SoA, 20) + iLQR gains (AoS, 10) values per step;
   // the f32 fast kernel: its per-lane records for one chunk (dtmpc_fast.hip)
   const size_t gen = el * (size_t)horizon * 30 * (size_t)B;
-  const size_t fast = dtype == DTMPC_F32 ? tube_fast_workspace_bytes(horizon, B, lanes, chunk) : 0;
+  size_t fast = 0;
+  if (dtype == DTMPC_F32) {
+    fast = tube_fast_workspace_bytes(horizon, B, lanes, chunk);
+  } else {  // f64 records: at most tube_fast_chunk_max64 trajectories per launch chunk
+    const int64_t c64 = tube_fast_chunk_max64(horizon, lanes);
+    fast = tube_fast_workspace_bytes64(horizon, B, lanes, chunk < c64 ? chunk : c64);
+  }
   return gen > fast ? gen : fast;
 }
 
@@ -795,6 +801,7 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
   if (cfg->disturbance != 0 && cfg->disturbance != 1) return set_err(DTMPC_ERR_BAD_ARG, "bad disturbance mode");
   hipStream_t st = (hipStream_t)stream;
   if (tube_fast_eligible(dtype, spec, cfg)) return launch_tube_fast(spec, cfg, B, global_offset, step, S, w, st);
+  if (tube_fast_eligible64(dtype, spec, cfg)) return launch_tube_fast64(spec, cfg, B, global_offset, step, S, w, st);
   if (dtype == DTMPC_F32) return launch_tube<float>(spec, cfg, B, global_offset, step, S, w, st);
   if (dtype == DTMPC_F64) return launch_tube<double>(spec, cfg, B, global_offset, step, S, w, st);
   return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");

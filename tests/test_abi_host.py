@@ -125,7 +125,13 @@ def test_arguments_validated_before_any_device_call(lib):
     assert lib.dtmpc_tube_chunk(50, 3) == 0
     assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536, 1, c1) == max(4 * 50 * 30, per1) * 65536
     assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 4096, 4, c4) == per4 * 4096
-    assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 65536, 1, c1) == 8 * 50 * 30 * 65536
+    # f64 (csrc/dtmpc_fast64.hip): the same records in doubles, so twice the bytes and at most half the chunk
+    per1d, per4d = 2 * per1, 2 * per4
+    c1d, c4d = (0x7FFFFFFF // per1d) // 256 * 256, (0x7FFFFFFF // per4d) // 256 * 256
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 65536, 1, c1) == max(8 * 50 * 30, per1d) * 65536
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 4096, 4, c4) == per4d * 4096
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 1 << 20, 1, c1) == max(8 * 50 * 30 * (1 << 20), per1d * c1d)
+    assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 100000, 4, c4) == per4d * min(c4, c4d)
     # above 2^31 bytes of records the fast kernel runs in chunks: the workspace holds one chunk
     assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 1 << 22, 1, c1) == 4 * 50 * 30 * (1 << 22)
     assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 100000, 4, c4) == per4 * c4

@@ -702,8 +702,9 @@ def test_tube_reset_fused_matches_stepwise(dev, tag):
         assert torch.equal(outs[0][k], outs[1][k]), k
 
 
+@pytest.mark.parametrize("tag", ["f32", "f64"])
 @pytest.mark.parametrize("lanes", ["1", "2", "4"])
-def test_tube_step_fast_chunked_bitwise(dev, lanes, monkeypatch):
+def test_tube_step_fast_chunked_bitwise(dev, lanes, tag, monkeypatch):
     """The f32 fast kernel keeps its per-lane records in one buffer resource (< 2^31 bytes), so a batch
     whose records exceed that runs in chunks of trajectories (dtmpc_fast.hip tube_fast_chunk).  Forcing
     chunks of 256 (DTMPC_FAST_CHUNK) on a ragged batch of 700 = 256 + 256 + 188 must give bitwise the
@@ -717,15 +718,16 @@ def test_tube_step_fast_chunked_bitwise(dev, lanes, monkeypatch):
     st = dataclasses.replace(st, ilqr_nom=dataclasses.replace(st.ilqr_nom, tol=-1.0),
                              ilqr_aux=dataclasses.replace(st.ilqr_aux, tol=-1.0))
     B = 700
+    npdt, tdt = DT[tag]  # f64: the same kernel source instantiated in f64 (csrc/dtmpc_fast64.hip)
     rng = np.random.default_rng(5)
-    x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(np.float32)
+    x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(npdt)
     names = ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux", "theta", "status", "log", "partials")
     runs = []
     for chunk in (None, "256"):
         if chunk:
             monkeypatch.setenv("DTMPC_FAST_CHUNK", chunk)
-        m = TubeMPC(st, batch=B, device=dev, dtype=torch.float32, disturbance="philox", seed=4, write_log=True)
-        m.reset(_t(x, torch.float32, dev))
+        m = TubeMPC(st, batch=B, device=dev, dtype=tdt, disturbance="philox", seed=4, write_log=True)
+        m.reset(_t(x, tdt, dev))
         m.step()
         m.step()
         torch.cuda.synchronize()
@@ -735,8 +737,9 @@ def test_tube_step_fast_chunked_bitwise(dev, lanes, monkeypatch):
         assert torch.equal(runs[0][k], runs[1][k]), k
 
 
+@pytest.mark.parametrize("tag", ["f32", "f64"])
 @pytest.mark.parametrize("lanes", ["1", "2", "4"])
-def test_tube_step_fast_gamma0_records(dev, lanes, monkeypatch):
+def test_tube_step_fast_gamma0_records(dev, lanes, tag, monkeypatch):
     """gamma = 0 (the paper's DBaS) makes the column of K for the barrier state exactly zero, and the
     fast kernel then keeps K and k in one 32-byte record per step (dtmpc_fast.hip fk::Gains).  The
     general 40-byte records (DTMPC_FAST_G0=0) must give the same values -- an exact zero term dropped
@@ -755,14 +758,15 @@ def test_tube_step_fast_gamma0_records(dev, lanes, monkeypatch):
     st = dataclasses.replace(st, ilqr_nom=dataclasses.replace(st.ilqr_nom, tol=-1.0),
                              ilqr_aux=dataclasses.replace(st.ilqr_aux, tol=-1.0))
     B = 700
+    npdt, tdt = DT[tag]
     rng = np.random.default_rng(6)
-    x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(np.float32)
+    x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1).astype(npdt)
     names = ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux", "theta", "status", "log", "partials")
     runs = []
     for g0 in ("1", "0"):
         monkeypatch.setenv("DTMPC_FAST_G0", g0)
-        m = TubeMPC(st, batch=B, device=dev, dtype=torch.float32, disturbance="philox", seed=4, write_log=True)
-        m.reset(_t(x, torch.float32, dev))
+        m = TubeMPC(st, batch=B, device=dev, dtype=tdt, disturbance="philox", seed=4, write_log=True)
+        m.reset(_t(x, tdt, dev))
         m.step()
         m.step()
         torch.cuda.synchronize()
@@ -770,6 +774,41 @@ def test_tube_step_fast_gamma0_records(dev, lanes, monkeypatch):
     assert (runs[0]["status"] == 0).all()
     for k in runs[0]:
         assert torch.equal(runs[0][k], runs[1][k]), k
+
+
+@pytest.mark.parametrize("lanes", ["1", "2", "4"])
+def test_tube_step_fast64_vs_generic(dev, lanes, monkeypatch):
+    """The f64 instantiation of the fused kernel (csrc/dtmpc_fast64.hip) against the generic f64 kernel
+    (DTMPC_FAST64=0, tube_step_kernel<double>) from the same start, one closed-loop step at the paper
+    settings: the same algorithm in two roundings (FMA contraction in the backward pass, the fdlibm sin/cos
+    kernels against OCML's), so states, plans and log rows agree to 1e-8 relative to each trajectory's
+    largest entry on >= 99 % of trajectories (the chaotic obstacle-grazing ones aside, test_tube_step_vs_oracle's band).  One step:
+    the next one runs on the batch-mean theta, which the few chaotic trajectories' gradients dominate."""
+    from diff_tube_mpc_strict_pt.core import TubeMPC
+
+    monkeypatch.setenv("DTMPC_TUBE_LANES", lanes)
+    st = paper_setup()
+    B = 700
+    rng = np.random.default_rng(21)
+    x = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1)
+    names = ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux", "log")
+    runs = []
+    for fast in ("1", "0"):
+        monkeypatch.setenv("DTMPC_FAST64", fast)
+        m = TubeMPC(st, batch=B, device=dev, dtype=torch.float64, disturbance="philox", seed=5, write_log=True)
+        m.reset(_t(x, torch.float64, dev))
+        m.step()
+        torch.cuda.synchronize()
+        assert (m.status == 0).all()
+        runs.append({k: getattr(m, k).cpu().numpy() for k in names})
+    for k in names:
+        a, b = runs[0][k], runs[1][k]
+        a = a.reshape(-1, B) if a.ndim > 1 else a[None]
+        b = b.reshape(-1, B) if b.ndim > 1 else b[None]
+        e = np.abs(a - b).max(0) / (np.abs(b).max(0) + 1e-30)
+        frac = float((e <= 1e-8).mean())
+        print(f"[fast64 vs generic lanes={lanes}] {k}: {frac:.4f} within 1e-8, max {e.max():.3g}")
+        assert frac >= 0.99, (k, frac, np.sort(e)[-5:])
 
 
 @pytest.mark.parametrize("tag", ["f64", "f32"])
