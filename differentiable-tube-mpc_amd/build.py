@@ -19,7 +19,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f)
-        for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_fast64.hip", "dtmpc_fast_ilqr.hip", "dtmpc_fast_general.hip", "dtmpc_general.hip", "dtmpc_receding.hip",
+        for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_fast64.hip", "dtmpc_fast64_ilqr.hip", "dtmpc_fast64_general.hip", "dtmpc_fast_ilqr.hip", "dtmpc_fast_general.hip", "dtmpc_general.hip", "dtmpc_receding.hip",
                   "dtmpc_control.hip", "dtmpc_ocp.hip", "dtmpc_systems.hip")]
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solver.hpp", "dtmpc_general.hpp",
                                                  "dtmpc_host.hpp", "dtmpc_ls_pk.hpp")] + [

@@ -2684,6 +2684,7 @@ size_t FKN(ilqr_fast_workspace_bytes)(int N, int64_t B, int lanes) {
 bool FKN(ilqr_fast_eligible)(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf) {
   const char* e = getenv("DTMPC_FAST");
   if (e && e[0] == '0' && e[1] == 0) return false;
+  if (DTMPC_FAST_F64 && (e = getenv("DTMPC_FAST64")) && e[0] == '0' && e[1] == 0) return false;
   if (dtype != kFastDtype || !fast_spec_ok(sp) || c->wrap_angle) return false;
   return make_ilqr<real>(*cf).nc == FK_NS::NC;
 }
@@ -2770,6 +2771,7 @@ static int64_t general_fast_bytes_per_traj(int N) {
 bool FKN(general_fast_eligible)(int dtype, const dtmpc_spec* sp, const dtmpc_general_cfg* cf) {
   const char* e = getenv("DTMPC_FAST");
   if (e && e[0] == '0' && e[1] == 0) return false;
+  if (DTMPC_FAST_F64 && (e = getenv("DTMPC_FAST64")) && e[0] == '0' && e[1] == 0) return false;
   // the tightening s comes from theta-bar (spec.h_offset is not used by the general path)
   if (dtype != kFastDtype || sp->obs_aggregation != DTMPC_OBS_SMOOTHMIN || sp->n_obstacles < 1 ||
       sp->n_obstacles > 8 || sp->barrier_type != DTMPC_BARRIER_INVERSE)

@@ -426,9 +426,10 @@ static int launch_general(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int
   a.status = S->status;
   a.iters = S->iters;
   const int dtype = sizeof(T) == 4 ? DTMPC_F32 : DTMPC_F64;
-  if (general_fast_eligible(dtype, sp, cf)) {
+  const bool f32 = general_fast_eligible(dtype, sp, cf), f64 = !f32 && general_fast_eligible64(dtype, sp, cf);
+  if (f32 || f64) {
     int* sst = (int*)((char*)S->work + general_scratch_bytes(dtype, sp->horizon, B));
-    const int e = launch_general_solve_fast(sp, cf, B, S, sst, st);
+    const int e = f32 ? launch_general_solve_fast(sp, cf, B, S, sst, st) : launch_general_solve_fast64(sp, cf, B, S, sst, st);
     if (e) return e;
     a.sst = sst;
     hipLaunchKernelGGL((general_step_kernel<T, 1, true>), grid_for(B), dim3(kBlock), 0, st, s, cfn, cfa, a);

@@ -662,8 +662,7 @@ size_t dtmpc_ilqr_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t
   if (horizon < 1 || horizon > DTMPC_MAX_HORIZON || B < 1) return 0;
   if (lanes == 0) lanes = tube_lanes_default(B);
   if (lanes != 1 && lanes != 2 && lanes != 4) return 0;
-  if (dtype == DTMPC_F64) return 0;  // the generic kernel: no workspace
-  return ilqr_fast_workspace_bytes(horizon, B, lanes);
+  return dtype == DTMPC_F64 ? ilqr_fast_workspace_bytes64(horizon, B, lanes) : ilqr_fast_workspace_bytes(horizon, B, lanes);
 }
 
 int dtmpc_ilqr_solve_ws(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
@@ -681,6 +680,9 @@ int dtmpc_ilqr_solve_ws(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cos
   if (ilqr_fast_eligible(dtype, spec, cost, cfg))
     return launch_ilqr_fast(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, (signed char*)choices,
                             lanes, work, work_bytes, (hipStream_t)stream);
+  if (ilqr_fast_eligible64(dtype, spec, cost, cfg))
+    return launch_ilqr_fast64(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, (signed char*)choices,
+                              lanes, work, work_bytes, (hipStream_t)stream);
   return dtmpc_ilqr_solve(dtype, spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, choices, stream);
 }
 

@@ -173,7 +173,9 @@ def test_arguments_validated_before_any_device_call(lib):
     assert lib.dtmpc_ilqr_workspace_bytes(_abi.F32, 50, 65536, 1) == ip1 * 65536
     assert lib.dtmpc_ilqr_workspace_bytes(_abi.F32, 50, 1 << 20, 4) == ((0x7FFFFFFF // ip4) // 256 * 256) * ip4
     assert lib.dtmpc_ilqr_workspace_bytes(_abi.F32, 50, 4096, 3) == 0
-    assert lib.dtmpc_ilqr_workspace_bytes(_abi.F64, 50, 4096, 0) == 0
+    # f64 (csrc/dtmpc_fast64_ilqr.hip): the same records in doubles
+    assert lib.dtmpc_ilqr_workspace_bytes(_abi.F64, 50, 4096, 4) == 2 * ip4 * 4096
+    assert lib.dtmpc_ilqr_workspace_bytes(_abi.F64, 50, 65536, 0) == 2 * ip1 * 65536
     rc = lib.dtmpc_ilqr_solve_ws(_abi.F32, C.byref(spec), C.byref(cost), C.byref(st.ilqr_nom.to_c()), 4, 1, None, None,
                                  1, 1, 1, 1, None, 1, None, 3, None, 0, None)
     assert rc == _abi.ERR_BAD_ARG and b"lanes" in lib.dtmpc_last_error()

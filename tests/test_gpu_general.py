@@ -108,16 +108,16 @@ def test_general_closed_loop_vs_reference(dev, tag):
             assert close(th[1][SL[nm]], g[f"theta_nom_final_{nm}"], 1e-9, 1e-12), nm
 
 
-@pytest.mark.parametrize("tag,solver,gamma", [("f64", "generic", 0.3), ("f32", "fast", 0.3), ("f32", "generic", 0.3),
-                                               ("f32", "fast", 0.0)])
+@pytest.mark.parametrize("tag,solver,gamma", [("f64", "generic", 0.3), ("f64", "fast", 0.3), ("f64", "fast", 0.0),
+                                               ("f32", "fast", 0.3), ("f32", "generic", 0.3), ("f32", "fast", 0.0)])
 def test_general_step_batched_vs_oracle(dev, oracle_lib, tag, solver, gamma, monkeypatch):
     """Batched general step (B = 300, ragged) from starts spread over the obstacle field (relaxed
     barrier, alpha / gamma / tightening gradients exercised), non-trivial raw parameters, 2 steps:
     per-trajectory plans, the 24 gradient rows, the shared theta update (applied to the device's own
     batch sums) and the plant step, against the three oracle builds from the device's pre-step state.
-    f32 runs both solvers: the fused one (general_solve_fast_kernel: gamma != 0 gain records, the
-    tightened nominal barrier) and the generic kernel (DTMPC_FAST=0); raw gamma 0 (tanh 0 = 0 exactly) runs
-    the fused solver's gamma = 0 records in both solves."""
+    Both precisions run both solvers: the fused one (general_solve_fast_kernel: gamma != 0 gain records, the
+    tightened nominal barrier; f64: csrc/dtmpc_fast64_general.hip) and the generic kernel (DTMPC_FAST=0); raw
+    gamma 0 (tanh 0 = 0 exactly) runs the fused solver's gamma = 0 records in both solves."""
     from diff_tube_mpc_strict_pt.core import GeneralTubeMPC
     from diff_tube_mpc_strict_pt.core.problem import general_setup_from_config
 

@@ -166,14 +166,14 @@ DECISION_GATE_TUBE = {"f64": 0.99, "f32": 0.84}
 # from all three oracle builds (measured 0.945 on determinate trajectories, 0.79 overall; f64 >= 0.99)
 DECISION_GATE_TRACK = {"f64": 0.99, "f32": 0.92}
 
-@pytest.mark.parametrize("tag,variant", [("f64", "generic"), ("f32", "l4"), ("f32", "l2"), ("f32", "l1"),
-                                         ("f32", "generic")])
+@pytest.mark.parametrize("tag,variant", [("f64", "generic"), ("f64", "l4"), ("f64", "l2"), ("f64", "l1"),
+                                         ("f32", "l4"), ("f32", "l2"), ("f32", "l1"), ("f32", "generic")])
 def test_ilqr_batched_vs_oracle(dev, oracle_lib, tag, variant, monkeypatch):
     """Ragged batch (B = 1000) of random starts / warm starts; nominal cost with fixed iterations and
     with the tol exit, then a tracking solve of the oracle's nominal plans.  Each trajectory must agree
     with the oracle within max(base, 10 x the spread of the three oracle builds on that trajectory).
-    f32 runs the fused solver (dtmpc_ilqr_solve_ws) at 4 / 2 / 1 lanes per trajectory and the generic
-    kernel (DTMPC_FAST=0); f64 always the generic kernel.  The last backward pass's gains K, k are
+    Both precisions run the fused solver (dtmpc_ilqr_solve_ws; f64: csrc/dtmpc_fast64_ilqr.hip) at 4 / 2 / 1
+    lanes per trajectory and the generic kernel (DTMPC_FAST=0).  The last backward pass's gains K, k are
     checked too (the same per-trajectory band)."""
     from diff_tube_mpc_strict_pt.core import ilqr_solve, tracking_cost
 
