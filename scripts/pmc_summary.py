@@ -19,7 +19,9 @@ import sys
 from collections import defaultdict
 
 
-TUBE_KERNELS = ("tube_fast_kernel", "tube_step_kernel")
+# the f32 headline kernel only: dtmpc::fk:: (the f64 instantiation is dtmpc::fk64::, the generic f64 one
+# tube_step_kernel<double>; a default bench run launches both in its secondary legs)
+TUBE_KERNELS = ("fk::tube_fast_kernel", "tube_step_kernel<float")
 
 
 def _match(name, kern):

@@ -20,7 +20,7 @@ run() {
 BENCH="bench.py --no-cpu --no-steady"
 run rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $BENCH
 python3 scripts/trace_summary.py "$OUT/trace" "$OUT/trace_summary.json" --warmup 3 || exit 1
-SHORT="bench.py --steps 5 --warmup 1 --no-cpu --no-steady"
+SHORT="bench.py --steps 5 --warmup 1 --no-cpu --no-steady --no-extra"
 run rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 $SHORT
 run rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 $SHORT
 run rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d "$OUT/sq1" -o run --output-format csv -- python3 $SHORT

@@ -13,7 +13,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("trace")
 ap.add_argument("out")
 ap.add_argument("--warmup", type=int, required=True)
-ap.add_argument("--kernel", default="tube_fast_kernel")
+ap.add_argument("--kernel", default="fk::tube_fast_kernel")  # f32 (fk64:: is the f64 leg)
 ap.add_argument("--batch", type=int, default=65536)
 ap.add_argument("--algo-bytes", type=float, default=274324.0 * 65536)
 a = ap.parse_args()
