@@ -151,7 +151,7 @@ def cpu_baseline(setup, seconds_target: float = 15.0):
 def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup: int = 3, generic: bool = False):
     """BASELINE config 2: batched nominal DDP (Dubins n = 3, m = 2 + barrier state, T = 50) over B
     trajectories on one GPU -- dtmpc_ilqr_solve_ws (core.ddp.ilqr_solve's entry: the fused solver at the
-    default lane count; f64 runs the generic kernel) with the nominal target cost, 10 fixed iterations
+    default lane count, f32 and f64) with the nominal target cost, 10 fixed iterations
     (tol = -1), 7 line-search alphas, zero warm start; generic=True times dtmpc_ilqr_solve (the generic
     kernel) instead.  One step = one solve of the whole batch from the same x0 / V_init (the control tape
     is re-seeded inside the timed region: it is the in/out buffer)."""
@@ -179,6 +179,7 @@ def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup
     lanes = int(lib.dtmpc_tube_lanes(B))
     wb = int(lib.dtmpc_ilqr_workspace_bytes(code, N, B, lanes))
     work = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
+    fused = bool(lib.dtmpc_ilqr_fused_eligible(code, C.byref(spec), C.byref(cc), C.byref(ic)))  # the path that runs
 
     def solve():
         Us.copy_(U0)
@@ -190,7 +191,7 @@ def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup
         else:
             _lib.check(lib.dtmpc_ilqr_solve_ws(code, C.byref(spec), C.byref(cc), C.byref(ic), B, x0.data_ptr(), None,
                                                None, Xs.data_ptr(), Us.data_ptr(), Ks.data_ptr(), ks.data_ptr(),
-                                               iters.data_ptr(), status.data_ptr(), None, lanes, work.data_ptr(), wb,
+                                               iters.data_ptr(), status.data_ptr(), None, None, lanes, work.data_ptr(), wb,
                                                _lib.stream_of(x0)), "dtmpc_ilqr_solve_ws")
 
     for _ in range(warmup):
@@ -207,38 +208,75 @@ def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup
     return {"workload": f"BASELINE config 2: batched nominal DDP, {cfg.max_iter} fixed iterations (tol=-1), "
                         f"{len(cfg.line_search_alphas)} alphas, T={N}, zero warm start",
             "batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall,
-            "kernel": ("generic ilqr_kernel" if generic or wb == 0 else f"fused ilqr_fast_kernel, {lanes} lanes"),
+            "kernel": ("generic ilqr_kernel" if generic or not fused else f"fused ilqr_fast_kernel, {lanes} lanes"),
             "event_ms_median": float(np.median([a.elapsed_time(b) for a, b in ev])),
             "value": B * cfg.max_iter / wall, "unit": "DDP iters/s",
             "nonzero_status": int((status != 0).sum())}
 
 
-def tube_leg(dev, dtype_name: str, B: int, steps: int, warmup: int):
-    """The headline tube step (episode start) at another precision, one GPU, B trajectories."""
+def warm_up(step, warmup: int, dev, min_launches: int = 8, max_launches: int = 40, rel: float = 0.01) -> int:
+    """Untimed warm-up past the clock ramp (the first launches of a fresh box ramp from
+    ~4.3 to ~4.05 ms): at least max(warmup, min_launches) steps, then more until two consecutive steps'
+    HIP-event times agree within `rel`, at most max_launches.  Returns the number run."""
+    n, last = 0, None
+    while True:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        step()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        n += 1
+        t = e0.elapsed_time(e1)
+        if n >= max(warmup, min_launches) and last is not None and abs(t - last) <= rel * last:
+            return n
+        if n >= max_launches:
+            return n
+        last = t
+
+
+def roofline_of(algo_bytes: float, kernel_ms: float, traffic=None, traffic_src=None) -> dict:
+    achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "algo_bytes_per_launch": algo_bytes}
+
+
+def tube_leg(dev, dtype_name: str, B: int, steps: int, warmup: int, adapt: bool = True, workload: str = ""):
+    """The tube step (episode start) on one GPU, B trajectories, in f32 or f64: the headline's other
+    precision, and BASELINE configs 3 (adapt=False: nominal + ancillary tube MPC, theta held) and 4 (the
+    same step with the IFT adaptation update of Algorithm 2) at B = 4,096.  roofline: SURVEY §8d's 274,324
+    algorithmic bytes per trajectory in f32 (x 2 in f64) over the fused kernel's HIP-event time."""
     dt = torch.float32 if dtype_name == "f32" else torch.float64
     setup = bench_setup(dtype_name)
     mpc = TubeMPC(setup, batch=B, device=dev, dtype=dt, disturbance="philox", seed=0, global_offset=0,
                   global_batch=B, process_group=None)
     x0 = initial_states(0, B, dev, dt)
-    for _ in range(warmup):
+
+    def one(k=None):
         mpc.reset(x0)
-        mpc.step()
-    torch.cuda.synchronize(dev)
+        mpc.step(kernel_events=k, adapt=adapt)
+
+    nwarm = warm_up(one, warmup, dev)
     kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
     for k in kev:
-        mpc.reset(x0)
-        mpc.step(kernel_events=k)
+        one(k)
     torch.cuda.synchronize(dev)
     wall = (time.perf_counter() - t0) / steps
-    out = {"batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall,
-           "kernel_ms": float(np.mean([a.elapsed_time(b) for a, b in kev])),
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
+    algo = ALGO_BYTES_PER_TRAJ_STEP * B * (2 if dtype_name == "f64" else 1)
+    traffic, src = pmc_traffic(B, kernel="tube" if dtype_name == "f32" else "tube_f64")
+    out = {"batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall, "warmup_run": nwarm,
+           "kernel_ms": kern_ms, "adapt": adapt,
            "value": B * ITERS_PER_STEP / wall, "unit": "DDP+IFT iters/s",
+           "roofline": roofline_of(algo, kern_ms, traffic, src),
            "flagged_trajectories": int((mpc.status != 0).sum()), "lanes": mpc.lanes,
            # the fused kernel in this precision (f64: csrc/dtmpc_fast64.hip) unless switched off for A/B
            "kernel": ("generic tube_step_kernel"
                       if os.environ.get("DTMPC_FAST") == "0" or (dtype_name == "f64" and os.environ.get("DTMPC_FAST64") == "0")
                       else "fused tube_fast_kernel")}
+    if workload:
+        out["workload"] = workload
     del mpc
     torch.cuda.empty_cache()
     return out
@@ -345,8 +383,19 @@ def main() -> None:
             dist.barrier()
             sync()
 
-    for _ in range(args.warmup):
-        step()
+    if args.dry_run:
+        for _ in range(args.warmup):
+            step()
+        nwarm = args.warmup
+    else:
+        nwarm = warm_up(step, args.warmup, dev)
+    # every rank warms up at least as long as the slowest (the same count keeps the ranks in step)
+    if world > 1:
+        wt = torch.tensor([nwarm], dtype=torch.int64, device=dev)
+        dist.all_reduce(wt, op=dist.ReduceOp.MAX)
+        for _ in range(int(wt) - nwarm):
+            step()
+        nwarm = int(wt)
     barrier()
     if args.dry_run:
         ev = kev = None
@@ -405,9 +454,9 @@ def main() -> None:
 
     ms_per_step = 1e3 * wall / args.steps
     value = Bg * ITERS_PER_STEP / (wall / args.steps)
-    algo_bytes = ALGO_BYTES_PER_TRAJ_STEP * (hi - lo)
-    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = (None, "dry run") if args.dry_run else pmc_traffic(hi - lo)
+    algo_bytes = ALGO_BYTES_PER_TRAJ_STEP * (hi - lo) * (2 if args.dtype == "f64" else 1)
+    traffic, traffic_src = ((None, "dry run") if args.dry_run
+                            else pmc_traffic(hi - lo, kernel="tube" if args.dtype == "f32" else "tube_f64"))
     out = {
         "metric": "DDP+IFT iters/sec, batched Dubins+DBaS T=50",
         "value": value,
@@ -431,13 +480,8 @@ def main() -> None:
         "kernel_ms_max_over_ranks": kern_ms_max,
         "flagged_trajectories": int(cnt[0]),
         "event_ms_per_step_median": float(np.median(step_ms)),
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "algo_bytes_per_launch": algo_bytes,
-        },
+        "warmup_run": nwarm,
+        "roofline": roofline_of(algo_bytes, kern_ms, traffic, traffic_src),
     }
     out["steady_state"] = steady
     if world == 1 and not args.dry_run and not args.no_extra:
@@ -447,6 +491,14 @@ def main() -> None:
         del mpc
         torch.cuda.empty_cache()
         out[f"tube_{other}"] = tube_leg(dev, other, Bg, steps=min(args.steps, 5), warmup=1)
+        # BASELINE configs 3 and 4 (one GPU, B = 4,096, f32): the tube MPC with theta held, and the same step
+        # with the IFT adaptation update
+        out["config3_tube_b4096"] = tube_leg(dev, "f32", 4096, steps=args.steps, warmup=args.warmup, adapt=False,
+                                             workload="BASELINE config 3: tube MPC (nominal 10 + ancillary 20 "
+                                                      "fixed iterations, DBaS), theta held, B=4096, episode start")
+        out["config4_adapt_b4096"] = tube_leg(dev, "f32", 4096, steps=args.steps, warmup=args.warmup, adapt=True,
+                                              workload="BASELINE config 4: the config-3 step + IFT sensitivity, "
+                                                       "DOC gradient and theta update (Algorithm 2), B=4096")
         out["nominal_ddp"] = {d: nominal_ddp_leg(dev, d, B=4096, steps=args.steps, warmup=args.warmup)
                               for d in ("f32", "f64")}
         out["nominal_ddp"]["f32_generic"] = nominal_ddp_leg(dev, "f32", B=4096, steps=args.steps,
@@ -457,6 +509,12 @@ def main() -> None:
         out["cpu_baseline"] = cpu_baseline(setup)
     else:
         out["cpu_baseline"] = None
+    # the reference's own PyTorch CPU path, measured in the build container (it cannot travel to the GPU
+    # box): SURVEY.md §6 / BASELINE.md, 8 processes x 1 thread, fixed-iteration tube steps
+    out["reference_cpu_container"] = {"f32": 18.3, "f64": 23.6, "unit": "DDP+IFT iters/s", "cores": 8,
+                                      "where": "build container (8 Xeon cores), not this box: the reference "
+                                               "itself (PyTorch, 8 processes x 1 thread)",
+                                      "source": "SURVEY.md §6, BASELINE.md"}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -127,6 +127,7 @@ struct FArgs {
   int stagger;  // s_sleep(127) rounds before this workgroup starts (phase desynchronisation, see launch)
   signed char* choices;  // [nom max_iter + aux max_iter][B] or NULL (dtmpc_tube_state.choices)
   real gbound;          // health bound on the gradient row (dtmpc_tube_cfg.grad_bound; +inf: none)
+  real* costs;          // [nom max_iter + aux max_iter][8][B] or NULL (dtmpc_tube_state.costs)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -280,7 +281,10 @@ struct GainLds {
 #ifndef DTMPC_FAST_LDS_STEPS
 #define DTMPC_FAST_LDS_STEPS 0
 #endif
-  static constexpr int KL = (!G0 || DTMPC_FAST_F64) ? 0 : kLdsF4 / (LS * Q) < DTMPC_FAST_LDS_STEPS ? kLdsF4 / (LS * Q) : DTMPC_FAST_LDS_STEPS;
+#ifndef DTMPC_FAST_LDS_GENERAL
+#define DTMPC_FAST_LDS_GENERAL 0  // 1: the general 40-byte records in LDS too (round-4 root-cause experiment)
+#endif
+  static constexpr int KL = ((!G0 && !DTMPC_FAST_LDS_GENERAL) || DTMPC_FAST_F64) ? 0 : kLdsF4 / (LS * Q) < DTMPC_FAST_LDS_STEPS ? kLdsF4 / (LS * Q) : DTMPC_FAST_LDS_STEPS;
   static constexpr bool used = KL > 0;
 };
 
@@ -1432,7 +1436,7 @@ __device__ __forceinline__ int gswap(int v) { return __builtin_amdgcn_mov_dpp(v,
 template <bool TRACK, int M, int P, class SV>
 __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FIlqr& cf, const real* x0, real Bc0,
                                            const SV& S, real Jprev, int h, real& bestJ, real& al_out, int& bc,
-                                           const Slots& Z) {
+                                           const Slots& Z, real* crec, size_t cst) {
   DTMPC_NOCONTRACT
   constexpr int NL = P == 4 ? 2 : SV::nc / P;  // candidates of this lane
   constexpr int NPR = (NL + 1) / 2;        // pairs
@@ -1527,6 +1531,17 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
     Jc[2 * q] = Jt.x;
     Jc[2 * q + 1] = Jt.y;
     ok = ok && vfinite(Jt);
+  }
+  // the candidate-cost record (diagnostics: the costs behind the decision; P = 4: lane 3 repeats lane 2)
+  if (crec) {
+#pragma unroll
+    for (int a = 0; a < NL; ++a) {
+      const int pos = P == 1 ? cf.cpos[a]
+                    : P == 2 ? (h ? cf.cpos[NL + a] : cf.cpos[a])
+                             : pick3(hc, cf.cpos[a], cf.cpos[2 + a], cf.cpos[4 + a]);
+      if (P != 4 || h < 3) crec[(size_t)pos * cst] = Jc[a];
+    }
+    if (cf.zpos >= 0 && h == 0) crec[(size_t)cf.zpos * cst] = Jprev;
   }
   // this lane's first strict minimum (its candidates are in increasing original order)
   real bJ = Jc[0];
@@ -1720,15 +1735,30 @@ struct SlotMap {
 constexpr int kSlots = 12;     // two banks of the six rolled-out candidates
 constexpr int kSlotInit = 6;   // the initial rollout: bank 1, so the first line search writes bank 0
 
+// the decision record of one solve (dtmpc_tube_state.choices / .costs, dtmpc_ilqr_solve_ws): this
+// trajectory's column of the winning-alpha record ch [max_iter][B] and of the candidate-cost record
+// cr [max_iter][8][B] (every line-search candidate's cost by original alpha position; the caller pre-fills
+// it, NaN: not run),
+// s = B (the column stride); either pointer may be null
+struct DecRec {
+  signed char* ch;
+  real* cr;
+  size_t s;
+};
+
 // iLQR for one trajectory (ilqr_traj, core/ddp.py:102-307).  P = 4: no commit pass -- the line search
 // kept every candidate's tape (Slots) and the winner's slot becomes the current tape (S.XA / S.UA).
 template <bool TRACK, int M, int P, bool SHIFT = true, class SV>
 __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf, const real* x0,
-                                    SV& S, int h, const SlotMap& sm, int& iters, Prof& pf, signed char* ch,
-                                    size_t chs) {
+                                    SV& S, int h, const SlotMap& sm, int& iters, Prof& pf, const DecRec& dr) {
   constexpr int ph = TRACK ? 4 : 0;  // phase-timer slots (profiling builds)
+  signed char* const ch = dr.ch;
+  const size_t chs = dr.s;
   if (ch && h == 0)  // the decision record: -1 for iterations not run (dtmpc_tube_state.choices)
     for (int it = 0; it < cf.max_iter; ++it) ch[it * chs] = -1;
+  // (the candidate-cost record is written only where a candidate ran: the caller pre-fills it -- a fill loop
+  // here made the f64 M = 3 tube kernel hit an AMDGPU back-end error, "Illegal instruction detected:
+  // V_CMP_NE_U32 0, src_private_base", ROCm 7.2 hipcc)
   real Jcur = init_tape<TRACK, M>(p, c, x0, S, cf.zpos >= 0 && cf.max_iter > 0);
   const real Bc0 = barrier_at<M>(p, x0[0], x0[1]);
   bool have_prev = false;
@@ -1755,7 +1785,8 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
       Z.U0 = RA{S.UA.base, S.UA.rs, sm.bu + q0 * sm.su};
       Z.U1 = RA{S.UA.base, S.UA.rs, sm.bu + (q0 + 1) * sm.su};
     }
-    const int best = line_search<TRACK, M, P>(p, c, cf, x0, Bc0, S, Jcur, h, bestJ, al, bc, Z);
+    const int best = line_search<TRACK, M, P>(p, c, cf, x0, Bc0, S, Jcur, h, bestJ, al, bc, Z,
+                                              dr.cr ? dr.cr + (size_t)it * 8 * chs : nullptr, chs);
     pf.mark(ph + 2);
 #ifdef DTMPC_PROFILE
     ls_stat(TRACK ? 1 : 0, best, al, cf);
@@ -2073,8 +2104,8 @@ tube_fast_kernel(FK kk) {
       const FCost cn = K->cn;
       const FIlqr cfn = K->cfn;
       const real xn0[4] = {y0, y1, y2, yb};
-      signed char* ch = K->a.choices ? K->a.choices + i : nullptr;
-      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, sm, itn, pf, ch, nb);
+      const DecRec dr{K->a.choices ? K->a.choices + i : nullptr, K->a.costs ? K->a.costs + i : nullptr, nb};
+      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, sm, itn, pf, dr);
     }
     FCost ca;  // ancillary weights theta (shared by the batch), terminal weight Qa (:885, :891)
     {
@@ -2103,8 +2134,9 @@ tube_fast_kernel(FK kk) {
       const FP p = phase_p<M>();
       const FIlqr cfa = K->cfa;
       const real xa0[4] = {x0, x1, x2, xb};
-      signed char* ch = K->a.choices ? K->a.choices + (size_t)K->cfn.max_iter * nb + i : nullptr;
-      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, sm, ita, pf, ch, nb);
+      const size_t o = (size_t)K->cfn.max_iter * nb + i;
+      const DecRec dr{K->a.choices ? K->a.choices + o : nullptr, K->a.costs ? K->a.costs + 8 * (o - i) + i : nullptr, nb};
+      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, sm, ita, pf, dr);
     }
     pf.mark(8);
     {  // upper loss, DOC sensitivity and gradient (:915-976)
@@ -2248,6 +2280,7 @@ struct IArgs {
   int* iters;
   int* status;
   signed char* choices;
+  real* costs;
   real* work;
   unsigned wsz, oX, oU, oK, ok, oXR, oUR;
 };
@@ -2310,16 +2343,19 @@ ilqr_fast_kernel(IK kk) {
   const real x0[4] = {a.x0[i], a.x0[nb + i], a.x0[2 * nb + i], a.x0[3 * nb + i]};
   const FCost c = ikargs()->c;
   const FIlqr cf = ikargs()->cf;
-  signed char* ch = a.choices ? a.choices + i : nullptr;
+  const DecRec dr{a.choices ? a.choices + i : nullptr, a.costs ? a.costs + i : nullptr, nb};
   int it = 0;
   Prof pf;
   pf.start();
-  const int st = ilqr<TRACK, M, P, false>(p, c, cf, x0, S, h, sm, it, pf, ch, nb);
-  // the last backward pass's gains out to the ABI arrays (G0 records: K's barrier column is exactly 0)
+  const int st = ilqr<TRACK, M, P, false>(p, c, cf, x0, S, h, sm, it, pf, dr);
+  // the last backward pass's gains out to the ABI arrays (G0 records: K's barrier column is exactly 0);
+  // max_iter = 0: no backward pass ran and the records were never written -- zeros, as the generic kernel
+  // leaves the zeroed arrays
+  const bool have_gains = cf.max_iter > 0;
   for (int k = h; k < N; k += P) {
-    f4 Ka, Kb;
-    f2 kf;
-    S.G.template load<G0>(S.r, k, Ka, Kb, kf);
+    f4 Ka = f4{0.f, 0.f, 0.f, 0.f}, Kb = f4{0.f, 0.f, 0.f, 0.f};
+    f2 kf = f2{0.f, 0.f};
+    if (have_gains) S.G.template load<G0>(S.r, k, Ka, Kb, kf);
     real* Kq = a.K + (size_t)k * 8 * nb + i;
     Kq[0] = Ka.x;
     Kq[nb] = Ka.y;
@@ -2406,7 +2442,7 @@ __device__ __forceinline__ int general_solve(const FP& p, const FCost& c, const 
   S.G = G;
   S.X = X;
   S.U = U;
-  const int st = ilqr<TRACK, M, P, false>(p, c, cf, x0, S, h, sm, it, pf, nullptr, 0);
+  const int st = ilqr<TRACK, M, P, false>(p, c, cf, x0, S, h, sm, it, pf, DecRec{nullptr, nullptr, 0});
   XA = S.XA;
   UA = S.UA;
   return st;
@@ -2615,6 +2651,7 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
   a.iters = S->iters;
   a.w = (const real*)w;
   a.choices = (signed char*)S->choices;
+  a.costs = (real*)S->costs;
   a.gbound = cf->grad_bound > 0 ? real(cf->grad_bound) : real(__builtin_inf());
   a.disturbance = cf->disturbance;
   a.write_log = (cf->write_log && S->log) ? 1 : 0;
@@ -2716,7 +2753,7 @@ bool FKN(ilqr_fast_eligible)(int dtype, const dtmpc_spec* sp, const dtmpc_cost* 
 
 int FKN(launch_ilqr_fast)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, const void* x0,
                      const void* Xref, const void* Uref, void* X, void* U, void* K, void* kff, int* iters, int* status,
-                     signed char* choices, int lanes, void* work, size_t work_bytes, hipStream_t st) {
+                     signed char* choices, void* costs, int lanes, void* work, size_t work_bytes, hipStream_t st) {
   const int N = sp->horizon;
   if (lanes != 1 && lanes != 2 && lanes != 4) return set_err(DTMPC_ERR_BAD_ARG, "lanes must be 1, 2 or 4");
   if (!work || work_bytes < FKN(ilqr_fast_workspace_bytes)(N, B, lanes))
@@ -2741,6 +2778,7 @@ int FKN(launch_ilqr_fast)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmp
   a.iters = iters;
   a.status = status;
   a.choices = choices;
+  a.costs = (real*)costs;
   a.work = (real*)work;
   // gamma = 0: the compact gain records and the Riccati step without the barrier state's column
   const int g0 = kk.p.gamma == 0.f ? 2 : 0;

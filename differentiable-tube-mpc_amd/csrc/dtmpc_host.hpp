@@ -195,13 +195,13 @@ bool ilqr_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, co
 size_t ilqr_fast_workspace_bytes(int N, int64_t B, int lanes);
 int launch_ilqr_fast(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, const void* x0,
                      const void* Xref, const void* Uref, void* X, void* U, void* K, void* kff, int* iters, int* status,
-                     signed char* choices, int lanes, void* work, size_t work_bytes, hipStream_t st);
+                     signed char* choices, void* costs, int lanes, void* work, size_t work_bytes, hipStream_t st);
 // ... and in f64 (dtmpc_fast64_ilqr.hip)
 bool ilqr_fast_eligible64(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf);
 size_t ilqr_fast_workspace_bytes64(int N, int64_t B, int lanes);
 int launch_ilqr_fast64(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, const void* x0,
                        const void* Xref, const void* Uref, void* X, void* U, void* K, void* kff, int* iters, int* status,
-                       signed char* choices, int lanes, void* work, size_t work_bytes, hipStream_t st);
+                       signed char* choices, void* costs, int lanes, void* work, size_t work_bytes, hipStream_t st);
 // the general path's two solves on the same solver (dtmpc_general_step); per-trajectory solve status to sst
 bool general_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_general_cfg* cf);
 int launch_general_solve_fast(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int64_t B,

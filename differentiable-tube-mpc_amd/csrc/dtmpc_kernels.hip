@@ -665,11 +665,17 @@ size_t dtmpc_ilqr_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t
   return dtype == DTMPC_F64 ? ilqr_fast_workspace_bytes64(horizon, B, lanes) : ilqr_fast_workspace_bytes(horizon, B, lanes);
 }
 
+int32_t dtmpc_ilqr_fused_eligible(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
+                                  const dtmpc_ilqr_cfg* cfg) {
+  if (!spec || !cost || !cfg) return 0;
+  return (ilqr_fast_eligible(dtype, spec, cost, cfg) || ilqr_fast_eligible64(dtype, spec, cost, cfg)) ? 1 : 0;
+}
+
 int dtmpc_ilqr_solve_ws(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
                         const dtmpc_ilqr_cfg* cfg, int64_t B, const void* x0, const void* Xref,
                         const void* Uref, void* X, void* U, void* K, void* kff, int32_t* iters,
-                        int32_t* status, int8_t* choices, int32_t lanes, void* work, size_t work_bytes,
-                        void* stream) {
+                        int32_t* status, int8_t* choices, void* costs, int32_t lanes, void* work,
+                        size_t work_bytes, void* stream) {
   int e = check_spec(spec, B);
   if (e) return e;
   if ((e = check_cost(cost, Xref, Uref))) return e;
@@ -679,10 +685,10 @@ int dtmpc_ilqr_solve_ws(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cos
   if (lanes != 1 && lanes != 2 && lanes != 4) return set_err(DTMPC_ERR_BAD_ARG, "lanes must be 0, 1, 2 or 4");
   if (ilqr_fast_eligible(dtype, spec, cost, cfg))
     return launch_ilqr_fast(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, (signed char*)choices,
-                            lanes, work, work_bytes, (hipStream_t)stream);
+                            costs, lanes, work, work_bytes, (hipStream_t)stream);
   if (ilqr_fast_eligible64(dtype, spec, cost, cfg))
     return launch_ilqr_fast64(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, (signed char*)choices,
-                              lanes, work, work_bytes, (hipStream_t)stream);
+                              costs, lanes, work, work_bytes, (hipStream_t)stream);
   return dtmpc_ilqr_solve(dtype, spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, choices, stream);
 }
 

@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_OBS = 16
 MAX_ALPHAS = 8
 MAX_HORIZON = 512
@@ -120,6 +120,7 @@ class DtmpcTubeState(C.Structure):
         ("chunk", C.c_int64),
         ("work_bytes", C.c_int64),
         ("choices", C.c_void_p),
+        ("costs", C.c_void_p),
     ]
 
 
@@ -190,10 +191,11 @@ PROTOTYPES = {
          P],
     ),
     "dtmpc_ilqr_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64, I32]),
+    "dtmpc_ilqr_fused_eligible": (I32, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg)]),
     "dtmpc_ilqr_solve_ws": (
         C.c_int,
         [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, P, P, P, P, P, P, P, P, P, P,
-         I32, P, C.c_size_t, P],
+         P, I32, P, C.c_size_t, P],
     ),
     "dtmpc_sensitivity_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64, I32]),
     "dtmpc_ddp_sensitivity": (

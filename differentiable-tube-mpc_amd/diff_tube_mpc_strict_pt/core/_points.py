@@ -1,7 +1,15 @@
 """Shared plumbing of the per-point entry points (include/dtmpc_systems.h): batch flattening, dtype /
 device checks and the launch.  Every array is point-major [n, F] (the reference's [B, F] layout), so a
 caller's tensor goes to the kernel as is when it is already contiguous.  There is no CPU fallback:
-host tensors raise ValueError, a missing library NativeLibraryError."""
+host tensors raise ValueError, a missing library NativeLibraryError.
+
+Autograd: the reference's per-function API is plain torch, so autograd differentiates through it (its
+``core/ddp.py`` ``_linearize_autograd`` and ``core/autodiff.py`` rely on that).  The functions whose
+reference bodies are differentiable maps -- ``dubins_step``, the h aggregations, the barriers and the box
+clamp -- are ``torch.autograd.Function``s here whose backward uses the analytic derivative the library
+already computes (the kernels' grad h / dB outputs, the Dubins Jacobian).  Every other entry point
+(Jacobians, cost derivatives, the tanh map) refuses an input that requires grad while grad mode is on
+(``require_device``), so a caller never gets an output silently cut from the graph."""
 from __future__ import annotations
 
 import ctypes as C
@@ -24,9 +32,21 @@ def dtype_code(t: Tensor) -> int:
 
 
 def require_device(*ts: Optional[Tensor]) -> None:
+    """Device tensors only; and no input that autograd would have to differentiate (see the module
+    docstring: the differentiable entry points call this inside their autograd.Function's forward,
+    where grad mode is off)."""
     for t in ts:
         if t is not None and t.device.type != "cuda":
             raise ValueError("the dtmpc HIP path needs device tensors (got %s); there is no CPU fallback" % t.device)
+    forbid_grad(*ts)
+
+
+def forbid_grad(*ts) -> None:
+    if torch.is_grad_enabled() and any(isinstance(t, Tensor) and t.requires_grad for t in ts):
+        raise RuntimeError("this dtmpc entry point is a HIP kernel without an autograd formula and an input "
+                           "requires grad: its output would be cut from the graph.  Differentiate through "
+                           "dubins_step / h_* / the barriers / BoxClampControl.clamp (autograd Functions), or "
+                           "call under torch.no_grad() / with detached inputs")
 
 
 def rows(t: Tensor, F: int, like: Tensor) -> Tuple[Tensor, Tuple[int, ...]]:
@@ -41,6 +61,7 @@ def rows(t: Tensor, F: int, like: Tensor) -> Tuple[Tensor, Tuple[int, ...]]:
 def scalar(v) -> float:
     """A float or a one-element tensor (the reference's ScalarLike)."""
     if isinstance(v, Tensor):
+        forbid_grad(v)
         if v.numel() != 1:
             raise NotImplementedError("per-point (batched) DBaS parameters are not supported; pass a scalar")
         return float(v.reshape(()).item())

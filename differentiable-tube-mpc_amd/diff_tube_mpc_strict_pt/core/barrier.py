@@ -4,7 +4,8 @@ The barrier functions evaluate in the HIP kernel of ``dtmpc_barrier_eval`` (incl
 elementwise over tensors of any shape on a HIP device; ``dbas_step`` / ``dbas_init_b0`` take the
 reference's callables f and h (evaluated as given -- the package's own ``systems.dubins.dubins_step``
 and ``systems.dubins_obstacles.h_*`` are device kernels) and combine them with the device barrier.
-There is no CPU fallback.  The fused solver kernels use the same device barrier code
+There is no CPU fallback.  B is differentiable (autograd, first order, through the kernel's dB), so
+``dbas_step`` composed with the package's differentiable ``dubins_step`` and ``h_*`` is too.  The fused solver kernels use the same device barrier code
 (``dtmpc_device.hpp`` barrier_relaxed / barrier_dyn).
 """
 from __future__ import annotations
@@ -35,11 +36,7 @@ class DBaSConfig:
     eps: float = 1e-6
 
 
-def barrier_and_derivative(zeta: Tensor, *, kind: int, alpha: float = 0.0, eps: float = 1e-12, want_B: bool = True,
-                           want_dB: bool = False):
-    """(B(zeta), dB/dzeta) of one barrier kind of ``dtmpc_barrier_eval`` (either may be skipped: None)."""
-    P.require_device(zeta)
-    z = zeta.contiguous()
+def _barrier_launch(z: Tensor, kind: int, alpha: float, eps: float, want_B: bool, want_dB: bool):
     n = z.numel()
     Bz = torch.empty_like(z) if want_B else None
     dBz = torch.empty_like(z) if want_dB else None
@@ -47,6 +44,34 @@ def barrier_and_derivative(zeta: Tensor, *, kind: int, alpha: float = 0.0, eps: 
         P.launch("dtmpc_barrier_eval", P.dtype_code(z), int(kind), float(alpha), float(eps), n, z.data_ptr(),
                  P.ptr(Bz), P.ptr(dBz), P.stream(z))
     return Bz, dBz
+
+
+class _Barrier(torch.autograd.Function):
+    """B(zeta) as an autograd node: backward dL/dzeta = dL/dB dB/dzeta with dB from the same launch (the
+    reference's barriers are torch expressions, core/barrier.py:36-72).  First order only."""
+
+    @staticmethod
+    def forward(ctx, zeta: Tensor, kind: int, alpha: float, eps: float):
+        P.require_device(zeta)
+        Bz, dBz = _barrier_launch(zeta.contiguous(), kind, alpha, eps, True, True)
+        ctx.save_for_backward(dBz)
+        return Bz
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g: Tensor):
+        (dBz,) = ctx.saved_tensors
+        return g * dBz, None, None, None
+
+
+def barrier_and_derivative(zeta: Tensor, *, kind: int, alpha: float = 0.0, eps: float = 1e-12, want_B: bool = True,
+                           want_dB: bool = False):
+    """(B(zeta), dB/dzeta) of one barrier kind of ``dtmpc_barrier_eval`` (either may be skipped: None).
+    B alone of an input that requires grad is an autograd node (_Barrier); dB is not differentiable."""
+    if want_B and not want_dB and torch.is_grad_enabled() and zeta.requires_grad:
+        return _Barrier.apply(zeta, int(kind), float(alpha), float(eps)), None
+    P.require_device(zeta)
+    return _barrier_launch(zeta.contiguous(), kind, alpha, eps, want_B, want_dB)
 
 
 def relaxed_inverse_barrier_B_alpha(zeta: Tensor, *, alpha: ScalarLike, eps: float = 1e-12) -> Tensor:

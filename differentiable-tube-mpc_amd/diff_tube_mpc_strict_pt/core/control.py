@@ -65,12 +65,34 @@ class BoxClampControl:
         return out.squeeze(0) if unbatched else out
 
     def clamp(self, u: Tensor) -> Tensor:
-        """core/control.py:61-64: torch.clamp(u, u_min, u_max) (NaN propagates)."""
+        """core/control.py:61-64: torch.clamp(u, u_min, u_max) (NaN propagates).  Differentiable like
+        torch.clamp (_BoxClamp: the gradient passes where u_min <= u <= u_max)."""
+        if torch.is_grad_enabled() and u.requires_grad:
+            return _BoxClamp.apply(u, self)
         return self._eval(u, True, False)
 
     def active_mask(self, u: Tensor) -> Tensor:
         """core/control.py:66-70: bool [..., 2], u within active_tol of a bound."""
         return self._eval(u, False, True)
+
+
+class _BoxClamp(torch.autograd.Function):
+    """BoxClampControl.clamp as an autograd node: forward the dtmpc_box_clamp kernel, backward torch.clamp's
+    rule (grad where u_min <= u <= u_max, 0 outside and for NaN), in torch ops on the saved input."""
+
+    @staticmethod
+    def forward(ctx, u: Tensor, box: "BoxClampControl"):
+        ctx.save_for_backward(u)
+        ctx.box = box
+        return box._eval(u, True, False)
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        (u,) = ctx.saved_tensors
+        lo, hi = _pair(ctx.box.u_min), _pair(ctx.box.u_max)
+        lo_t = torch.tensor(lo, dtype=u.dtype, device=u.device)
+        hi_t = torch.tensor(hi, dtype=u.dtype, device=u.device)
+        return g * ((u >= lo_t) & (u <= hi_t)).to(g.dtype), None
 
 
 @dataclass(frozen=True)

@@ -100,6 +100,7 @@ class ILQRResult:
     iters: Tensor  # [B] int32
     status: Tensor  # [B] int32
     choices: Optional[Tensor] = None  # [B, max_iter] int8: winning alpha position per iteration, -1 not run
+    costs: Optional[Tensor] = None  # [B, max_iter, 8]: every line-search candidate's cost by alpha position
 
 
 @dataclass(frozen=True)
@@ -170,14 +171,18 @@ def linearize(problem: DubinsDBaSProblem, cost: QuadraticCost, X: Tensor, V: Ten
 def ilqr_solve(*, problem: DubinsDBaSProblem, cost: QuadraticCost, cfg: ILQRConfig, x0: Tensor,
                V_init: Tensor, X_ref: Optional[Tensor] = None, U_ref: Optional[Tensor] = None,
                check: bool = True, debug_name: str = "ilqr", record_choices: bool = False,
-               lanes: int = 0) -> ILQRResult:
+               lanes: int = 0, record_costs: bool = False) -> ILQRResult:
     """Batched box-clamped iLQR (core/ddp.py:102-307).
 
     x0 [B, 4], V_init [B, N, 2] (not mutated), X_ref [B, N+1, >=3] / U_ref [B, N, 2] for the tracking
     cost.  Returns X* [B, N+1, 4], V* [B, N, 2] and diagnostics; record_choices adds the decision
-    record (the winning line-search alpha position of every iteration, core/ddp.py:293).
-    Runs dtmpc_ilqr_solve_ws: the tube step's fused solver on the paper configuration (f32) with
-    ``lanes`` lanes per trajectory (0: dtmpc_tube_lanes(B); 1, 2 or 4), else the generic kernel."""
+    record (the winning line-search alpha position of every iteration, core/ddp.py:293); record_costs
+    the costs behind it (every candidate's J by alpha position [B, max_iter, 8], NaN not run; fused
+    solver only -- None when the generic kernel runs).
+    Runs dtmpc_ilqr_solve_ws: the tube step's fused solver on the paper configuration (f32 and f64:
+    csrc/dtmpc_fast_ilqr.hip / dtmpc_fast64_ilqr.hip; DTMPC_FAST=0 / DTMPC_FAST64=0 switch it off) with
+    ``lanes`` lanes per trajectory (0: dtmpc_tube_lanes(B); 1, 2 or 4), else the generic kernel
+    (dtmpc_ilqr_fused_eligible says which)."""
     _require_device(x0, V_init, X_ref, U_ref)
     B, N = x0.shape[0], problem.horizon
     if cfg.horizon != N:
@@ -198,20 +203,24 @@ def ilqr_solve(*, problem: DubinsDBaSProblem, cost: QuadraticCost, cfg: ILQRConf
     iters = torch.zeros(B, dtype=torch.int32, device=x0.device)
     status = torch.zeros(B, dtype=torch.int32, device=x0.device)
     ch = torch.empty(max(cfg.max_iter, 1), B, dtype=torch.int8, device=x0.device) if record_choices else None
+    fused = bool(lib.dtmpc_ilqr_fused_eligible(_dtype_code(x0), C.byref(spec), C.byref(cc), C.byref(ic)))
+    cr = (torch.full((max(cfg.max_iter, 1), 8, B), float("nan"), **kw) if record_costs and fused else None)
     if lanes not in (0, 1, 2, 4):
         raise ValueError("lanes must be 0 (default), 1, 2 or 4")
     wb = int(lib.dtmpc_ilqr_workspace_bytes(_dtype_code(x0), N, B, lanes))
     work = torch.empty(max(wb, 1), dtype=torch.uint8, device=x0.device)
     _lib.check(lib.dtmpc_ilqr_solve_ws(_dtype_code(x0), C.byref(spec), C.byref(cc), C.byref(ic), B, x0s.data_ptr(),
                                        _ptr(Xr), _ptr(Ur), Xs.data_ptr(), Us.data_ptr(), Ks.data_ptr(), ks.data_ptr(),
-                                       iters.data_ptr(), status.data_ptr(), _ptr(ch), lanes, work.data_ptr(), wb,
+                                       iters.data_ptr(), status.data_ptr(), _ptr(ch), _ptr(cr), lanes,
+                                       work.data_ptr(), wb,
                                        _lib.stream_of(x0)),
                "dtmpc_ilqr_solve_ws")
     if check:
         raise_for_status(status, debug_name)
     return ILQRResult(X=from_soa(Xs), V=from_soa(Us), K=from_soa(Ks).view(B, N, 2, 4), k=from_soa(ks),
                       iters=iters, status=status,
-                      choices=ch[:cfg.max_iter].t().contiguous() if ch is not None else None)
+                      choices=ch[:cfg.max_iter].t().contiguous() if ch is not None else None,
+                      costs=cr[:cfg.max_iter].permute(2, 0, 1).contiguous() if cr is not None else None)
 
 
 def ddp_sensitivity(*, problem: DubinsDBaSProblem, cost: QuadraticCost, X: Tensor, V: Tensor,

@@ -30,21 +30,55 @@ class DubinsConfig:
     x_target: Tuple[float, float, float] = (10.0, 10.0, float(torch.pi / 4))
 
 
+def _dubins_launch(x3: Tensor, u: Tensor, dt: float) -> Tensor:
+    xr, lead = P.rows(x3, 3, x3)
+    ur, _ = P.rows(u, 2, x3)
+    out = torch.empty_like(xr)
+    if xr.shape[0] > 0:
+        P.launch("dtmpc_dubins_step", P.dtype_code(xr), P.byref(P.spec(dt=dt)), xr.shape[0], 3, xr.data_ptr(),
+                 ur.data_ptr(), out.data_ptr(), P.stream(xr))
+    return out.reshape(*lead, 3)
+
+
+class _DubinsStep(torch.autograd.Function):
+    """dubins_step as an autograd node: forward in the HIP kernel, backward the Dubins Jacobian
+    (core/systems/dubins_aug_jac.py:42-58, A3 = I + dt v [-sin, cos] in column theta, B3 = dt [[cos, 0],
+    [sin, 0], [0, 1]]) written in torch ops on the saved device inputs, so it is differentiable again (the
+    reference's autograd Hessians, core/autodiff.py:9-42)."""
+
+    @staticmethod
+    def forward(ctx, x3: Tensor, u: Tensor, dt: float) -> Tensor:
+        P.require_device(x3, u)
+        ctx.save_for_backward(x3, u)
+        ctx.dt = dt
+        return _dubins_launch(x3, u, dt)
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        x3, u = ctx.saved_tensors
+        dt = ctx.dt
+        s, c = torch.sin(x3[..., 2]), torch.cos(x3[..., 2])
+        g0, g1, g2 = g[..., 0], g[..., 1], g[..., 2]
+        gx = torch.stack([g0, g1, g2 + (dt * u[..., 0]) * (c * g1 - s * g0)], -1)
+        gu = torch.stack([dt * (c * g0 + s * g1), dt * g2], -1)
+        return gx, gu, None
+
+
 def dubins_step(x: Tensor, u: Tensor, *, cfg: DubinsConfig) -> Tensor:
-    """core/systems/dubins.py:24-43: [px + dt v cos(th), py + dt v sin(th), th + dt omega]."""
-    P.require_device(x, u)
+    """core/systems/dubins.py:24-43: [px + dt v cos(th), py + dt v sin(th), th + dt omega].
+    Differentiable (autograd) in x and u (_DubinsStep)."""
     unbatched = x.ndim == 1
     xs = x.unsqueeze(0) if unbatched else x
     us = u.unsqueeze(0) if u.ndim == 1 else u
     if xs.shape[-1] < 3:
         raise ValueError("x must be [..., 3] (px, py, theta)")
-    xr, lead = P.rows(xs[..., :3], 3, xs)
-    ur, _ = P.rows(us.expand(*lead, 2), 2, xs)
-    out = torch.empty_like(xr)
-    if xr.shape[0] > 0:
-        P.launch("dtmpc_dubins_step", P.dtype_code(xr), P.byref(P.spec(dt=cfg.dt)), xr.shape[0], 3, xr.data_ptr(),
-                 ur.data_ptr(), out.data_ptr(), P.stream(xr))
-    out = out.reshape(*lead, 3)
+    x3 = xs[..., :3]
+    ue = us.expand(*x3.shape[:-1], 2)
+    if torch.is_grad_enabled() and (x3.requires_grad or ue.requires_grad):
+        out = _DubinsStep.apply(x3, ue, float(cfg.dt))
+    else:
+        P.require_device(x3, ue)
+        out = _dubins_launch(x3, ue, float(cfg.dt))
     return out.squeeze(0) if unbatched else out
 
 

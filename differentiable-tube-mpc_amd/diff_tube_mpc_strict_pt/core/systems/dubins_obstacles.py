@@ -5,6 +5,7 @@ h_i(x) = ||p - c_i||^2 - r_i^2 aggregated as one circle, a smooth-min -(1/beta) 
 exact min, and their (sub)gradients, from the HIP kernel ``dtmpc_h_eval`` -- the device code the fused
 solver kernels use.  x is [..., >=2] on a HIP device (unbatched [3] gives a scalar h and a [3]
 gradient); the gradients also accept a batch (the reference's analytic gradients take one point).
+The h values are differentiable (autograd, first order) through the kernel's own gradient.
 """
 from __future__ import annotations
 
@@ -20,13 +21,9 @@ __all__ = ["CircleObstacle", "h_circle_obstacle", "grad_h_circle_obstacle", "h_m
            "grad_h_multi_circle_obstacles", "h_min_circle_obstacles", "grad_h_min_circle_obstacles"]
 
 
-def _h(x: Tensor, sp, want_grad: bool):
-    P.require_device(x)
-    unbatched = x.ndim == 1
-    xs = x.unsqueeze(0) if unbatched else x
+def _h_launch(xs: Tensor, sp, want_grad: bool):
+    """h [n] (and grad h [n, 3]) of the points xs [..., F >= 2] from dtmpc_h_eval, shaped like xs's batch."""
     F = xs.shape[-1]
-    if F < 2:
-        raise ValueError("x must hold (px, py, ...)")
     xr, lead = P.rows(xs, F, xs)
     n = xr.shape[0]
     h = torch.empty(n, dtype=xr.dtype, device=xr.device)
@@ -34,11 +31,43 @@ def _h(x: Tensor, sp, want_grad: bool):
     if n > 0:
         P.launch("dtmpc_h_eval", P.dtype_code(xr), P.byref(sp), n, F, xr.data_ptr(), h.data_ptr(), P.ptr(g),
                  P.stream(xr))
-    if want_grad:
-        g = g.reshape(*lead, 3)
-        return g.squeeze(0) if unbatched else g
-    h = h.reshape(lead)
-    return h.squeeze(0) if unbatched else h
+    return h.reshape(lead), (g.reshape(*lead, 3) if want_grad else None)
+
+
+class _HValue(torch.autograd.Function):
+    """h(x) as an autograd node: backward dL/dx = dL/dh grad h(x), grad h from the same kernel launch
+    (the reference's analytic gradients, core/systems/dubins_obstacles.py:33-38, 72-92, 109-117; the
+    exact min's argmin subgradient as torch.min's).  First order only (once_differentiable: a second
+    derivative of h raises)."""
+
+    @staticmethod
+    def forward(ctx, xs: Tensor, sp):
+        P.require_device(xs)
+        h, g = _h_launch(xs, sp, True)
+        F = xs.shape[-1]
+        gx = g[..., :F] if F <= 3 else torch.cat([g, g.new_zeros(*g.shape[:-1], F - 3)], -1)
+        ctx.save_for_backward(gx)
+        return h
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gh: Tensor):
+        (gx,) = ctx.saved_tensors
+        return gh.unsqueeze(-1) * gx, None
+
+
+def _h(x: Tensor, sp, want_grad: bool):
+    unbatched = x.ndim == 1
+    xs = x.unsqueeze(0) if unbatched else x
+    if xs.shape[-1] < 2:
+        raise ValueError("x must hold (px, py, ...)")
+    if not want_grad and torch.is_grad_enabled() and xs.requires_grad:
+        h = _HValue.apply(xs, sp)
+        return h.squeeze(0) if unbatched else h
+    P.require_device(xs)
+    h, g = _h_launch(xs, sp, want_grad)
+    out = g if want_grad else h
+    return out.squeeze(0) if unbatched else out
 
 
 def _agg_spec(obstacles: Sequence[CircleObstacle], agg: str, beta: float = 20.0):

@@ -92,6 +92,8 @@ class TubeMPC:
         (pass w to :meth:`step`).
       global_offset / global_batch: position of this shard in the global batch (multi-GPU).
       write_log: keep the per-step record (x, u, xbar, ubar, b, L, gQ, gR, gqb) on device.
+      record_costs: keep the costs behind those decisions (``costs`` [I_nom + I_aux, 8, B]: every
+        line-search candidate's cost by alpha position; fused kernels only).
       record_choices: keep the step's decision record (``choices`` [I_nom + I_aux, B] int8: the winning
         line-search alpha position of every nominal, then ancillary iteration, -1 not run).
       grad_bound: health policy of the shared update -- a trajectory whose DOC gradient row has a
@@ -103,7 +105,8 @@ class TubeMPC:
 
     def __init__(self, setup, *, batch: int, device="cuda", dtype=torch.float32, disturbance: str = "philox",
                  seed: int = 0, global_offset: int = 0, global_batch: Optional[int] = None, process_group=None,
-                 write_log: bool = False, record_choices: bool = False, grad_bound: Optional[float] = None):
+                 write_log: bool = False, record_choices: bool = False, grad_bound: Optional[float] = None,
+                 record_costs: bool = False):
         if isinstance(setup, dict):
             setup = paper_setup_from_config(setup)
         self.setup: PaperSetup = setup
@@ -169,6 +172,10 @@ class TubeMPC:
         nch = setup.ilqr_nom.max_iter + setup.ilqr_aux.max_iter
         self.choices = (torch.full((max(nch, 1), B), -1, dtype=torch.int8, device=self.device)
                         if record_choices else None)
+        # the costs behind the decisions: [I_nom + I_aux, 8, B] every candidate's J by alpha position (fused
+        # kernels only; NaN where not run)
+        self.costs = (torch.full((max(nch, 1), 8, B), float("nan"), dtype=dtype, device=self.device)
+                      if record_costs else None)
         self.t = 0
         st = _abi.DtmpcTubeState()
         st.x, st.b, st.xbar, st.bbar = (t.data_ptr() for t in (self.x, self.b, self.xbar, self.bbar))
@@ -184,6 +191,7 @@ class TubeMPC:
         st.chunk = self.chunk
         st.work_bytes = wbytes
         st.choices = self.choices.data_ptr() if self.choices is not None else None
+        st.costs = self.costs.data_ptr() if self.costs is not None else None
         self.state = st
 
     # -----------------------------------------------------------------------------------------
@@ -221,9 +229,12 @@ class TubeMPC:
     def _stream(self) -> int:
         return int(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def step(self, w: Optional[Tensor] = None, kernel_events=None) -> None:
+    def step(self, w: Optional[Tensor] = None, kernel_events=None, adapt: bool = True) -> None:
         """One closed-loop step for the whole batch (asynchronous on the current stream).
-        kernel_events: optional (start, end) torch.cuda.Event pair recorded around the fused kernel."""
+        kernel_events: optional (start, end) torch.cuda.Event pair recorded around the fused kernel.
+        adapt=False: theta is held (no partial-sum reduction, all-reduce or update) -- the tube MPC of
+        BASELINE config 3 without the adaptation step of config 4; the IFT pass still runs in the fused
+        kernel (its per-trajectory rows land in the log)."""
         wp = None
         if self.cfg.disturbance == 0:
             if w is None or w.shape != (self.B, 3):
@@ -231,6 +242,8 @@ class TubeMPC:
             self._w = w.to(device=self.device, dtype=self.dtype).t().contiguous()
             wp = self._w.data_ptr()
         s = self._stream()
+        if self.costs is not None:  # the kernel writes the candidates that ran: NaN marks the rest
+            self.costs.fill_(float("nan"))
         if kernel_events is not None:
             kernel_events[0].record()
         _lib.check(self.lib.dtmpc_tube_step(self._dt, C.byref(self.spec), C.byref(self.cfg), self.B,
@@ -238,6 +251,9 @@ class TubeMPC:
                    "dtmpc_tube_step")
         if kernel_events is not None:
             kernel_events[1].record()
+        if not adapt:
+            self.t += 1
+            return
         _lib.check(self.lib.dtmpc_partials_reduce(self._dt, self.n_partials, self.partials.data_ptr(),
                                                   self.sums.data_ptr(), s), "dtmpc_partials_reduce")
         allreduce_sums(self.sums, self.group)
@@ -261,6 +277,20 @@ class TubeMPC:
     def healthy_count(self) -> int:
         """Trajectories of the global batch that contributed to the last step's mean gradient."""
         return int(round(float(self.sums[_abi.TUBE_SUMS - 1])))
+
+    @property
+    def flagged_count(self) -> int:
+        """Trajectories of the global batch with a status flag (OR-accumulated over the episode)."""
+        n = torch.tensor([float((self.status != 0).sum())], dtype=torch.float64, device=self.status.device)
+        return int(round(float(allreduce_sums(n, self.group))))
+
+    @property
+    def bound_dropped_count(self) -> int:
+        """Trajectories of the global batch that the last step's mean gradient left out ONLY because of
+        the health bound: a gradient component above ``grad_bound`` or non-finite -- non-finite
+        rows are left out even with the bound disabled, since one NaN row would make the batch mean NaN --
+        i.e. the global batch minus the healthy and the flagged trajectories."""
+        return self.global_batch - self.healthy_count - self.flagged_count
 
     def nominal_tape(self):
         return self.Xnom.permute(2, 0, 1), self.Unom.permute(2, 0, 1)

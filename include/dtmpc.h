@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DTMPC_ABI_VERSION 4
+#define DTMPC_ABI_VERSION 5
 #define DTMPC_MAX_OBS 16
 #define DTMPC_MAX_ALPHAS 8
 #define DTMPC_MAX_HORIZON 512
@@ -144,7 +144,11 @@ typedef struct dtmpc_tube_cfg {
   double grad_bound;        /* health policy of the shared update: a trajectory whose DOC gradient row
                                [gQ, gR, gqb] has a component of magnitude above grad_bound (or a
                                non-finite one) drops out of the batch sums like a flagged trajectory;
-                               <= 0 disables the bound (only status flags exclude) */
+                               <= 0 disables the magnitude bound, but a row with a non-finite component
+                               is always left out (one NaN row would make the batch mean NaN).  The
+                               count left out this way is the global batch minus the healthy count
+                               (partials slot 7) minus the flagged trajectories (TubeMPC
+                               .bound_dropped_count) */
 } dtmpc_tube_cfg;
 
 /* Device-resident closed-loop state; all SoA [fields][B] unless stated, caller-owned. */
@@ -178,6 +182,12 @@ typedef struct dtmpc_tube_state {
                        step -- per iteration of the nominal, then the ancillary solve, the
                        original position of the winning line-search alpha (core/ddp.py:293, strict <,
                        first wins), -1 for iterations not run */
+  void* costs;      /* [nom_ilqr.max_iter + aux_ilqr.max_iter][8][B] (dtype) or NULL: the costs behind the
+                       decisions -- every line-search candidate's cost J (core/ddp.py:286-291) by
+                       original alpha position, the alpha = 0 candidate's the current tape's; only the
+                       candidates that ran are written (pre-fill it, e.g. with NaN).  Written by the fused
+                       kernels only (diagnostics / the tie-aware parity
+                       gate, tests/_common.py); the generic kernel leaves it untouched */
 } dtmpc_tube_state;
 
 int dtmpc_abi_version(void);
@@ -226,20 +236,32 @@ int dtmpc_ilqr_solve(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
                      void* stream);
 
 /* Workspace bytes of dtmpc_ilqr_solve_ws for B trajectories at `lanes` per trajectory (0: the
- * dtmpc_tube_lanes(B) default; 1, 2 or 4); 0 for bad arguments and for DTMPC_F64 (generic kernel). */
+ * dtmpc_tube_lanes(B) default; 1, 2 or 4), for DTMPC_F32 and DTMPC_F64 alike (both precisions have the
+ * fused solver: csrc/dtmpc_fast_ilqr.hip, csrc/dtmpc_fast64_ilqr.hip); 0 for bad arguments. */
 size_t dtmpc_ilqr_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t lanes);
 
 /* dtmpc_ilqr_solve (same arrays, same results contract) through the fused solver of the tube step
- * on the fast configuration -- f32, smooth-min obstacles (1..8), relaxed inverse barrier, h_offset 0,
- * no angle wrap, six non-zero line-search alphas (plus at most one alpha = 0) -- with `lanes` lanes per
+ * on the fast configuration -- f32 or f64, smooth-min obstacles (1..8), relaxed inverse barrier,
+ * h_offset 0, six non-zero line-search alphas (plus at most one alpha = 0) -- with `lanes` lanes per
  * trajectory (0: default) and a caller-owned workspace of dtmpc_ilqr_workspace_bytes; any other
- * configuration (and DTMPC_FAST=0 in the environment) runs dtmpc_ilqr_solve's generic kernel.
+ * configuration (DTMPC_FAST=0 in the environment, or DTMPC_FAST64=0 for f64) runs dtmpc_ilqr_solve's
+ * generic kernel (dtmpc_ilqr_fused_eligible says which).  costs (or NULL): [max_iter][8][B] every
+ * line-search candidate's cost by alpha position as dtmpc_tube_state.costs (fused solver only; only the
+ * candidates that ran are written).
+ * max_iter = 0: K and kff are written as zeros
+ * (no backward pass ran), as the generic kernel leaves the zeroed arrays the package passes.
  * Replaces core/ddp.py:102-307 `ilqr_solve` (the batched nominal DDP of BASELINE config 2). */
+/* 1 when dtmpc_ilqr_solve_ws runs the fused solver for this problem / cost / config in this precision
+ * (and the environment's DTMPC_FAST / DTMPC_FAST64 switches), 0 when it falls to dtmpc_ilqr_solve's
+ * generic kernel.  Host-only (no device call). */
+int32_t dtmpc_ilqr_fused_eligible(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
+                                  const dtmpc_ilqr_cfg* cfg);
+
 int dtmpc_ilqr_solve_ws(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
                         const dtmpc_ilqr_cfg* cfg, int64_t B, const void* x0,
                         const void* Xref, const void* Uref, void* X, void* U,
                         void* K, void* kff, int32_t* iters, int32_t* status, int8_t* choices,
-                        int32_t lanes, void* work, size_t work_bytes, void* stream);
+                        void* costs, int32_t lanes, void* work, size_t work_bytes, void* stream);
 
 /* Scratch bytes for dtmpc_ddp_sensitivity. */
 size_t dtmpc_sensitivity_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t want_lambda);

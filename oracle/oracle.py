@@ -157,9 +157,10 @@ class Oracle:
                                     _p(Xr), _p(Ur), _p(J))
         return J
 
-    def ilqr_solve(self, spec, cost, cfg, x0, V_init, Xref=None, Uref=None, choices=False):
+    def ilqr_solve(self, spec, cost, cfg, x0, V_init, Xref=None, Uref=None, choices=False, costs=False):
         """Returns X, V, K, k, iters, status, and with choices the decision record [B, max_iter] int8
-        (the winning alpha position of every iteration, -1 not run)."""
+        (the winning alpha position of every iteration, -1 not run), then with costs every line-search
+        candidate's cost [B, max_iter, 8] by alpha position (NaN: not run)."""
         x0 = self._a(x0)
         B, N = x0.shape[0], spec.horizon
         x0s = np.ascontiguousarray(x0.T)
@@ -172,11 +173,16 @@ class Oracle:
         iters = np.zeros(B, np.int32)
         status = np.zeros(B, np.int32)
         ch = np.full((max(cfg.max_iter, 1), B), -1, np.int8) if choices else None
+        cc = np.full((max(cfg.max_iter, 1), 8, B), np.nan, self.dt) if costs else None
         self._f("oracle_ilqr_solve_ex")(C.byref(spec), C.byref(cost), C.byref(cfg), C.c_longlong(B), _p(x0s), _p(Xr),
                                         _p(Ur), _p(Xs), _p(Us), _p(Ks), _p(ks), _p(iters), _p(status), _p(ch),
-                                        C.c_int(self.nthreads))
+                                        _p(cc), C.c_int(self.nthreads))
         out = (aos(Xs), aos(Us), aos(Ks).reshape(B, N, 2, 4), aos(ks), iters, status)
-        return out + (np.ascontiguousarray(ch[:cfg.max_iter].T),) if choices else out
+        if choices:
+            out = out + (np.ascontiguousarray(ch[:cfg.max_iter].T),)
+        if costs:
+            out = out + (np.ascontiguousarray(np.transpose(cc[:cfg.max_iter], (2, 0, 1))),)
+        return out
 
     def ddp_sensitivity(self, spec, cost, X, V, Xbar, want_lambda=True):
         X = self._a(X)
@@ -199,11 +205,12 @@ class Oracle:
         return np.ascontiguousarray(out.T)
 
     def tube_step(self, spec, tcfg, st: dict, theta, w=None, goff: int = 0, step: int = 0, want_log=True,
-                  choices=False):
+                  choices=False, costs=False):
         """One Algorithm-2 step for every trajectory; `st` holds SoA numpy arrays (x [3,B], b [B],
         xbar, bbar, Xnom [N+1,4,B], Unom [N,2,B], Xaux, Uaux) updated in place.  Returns per-trajectory
         [7, B] (L, gQ, gR, gqb), log [18, B], status [B], iters [2, B] (+ with choices the decision record
-        [I_nom + I_aux, B] int8: winning alpha position per iteration, -1 not run)."""
+        [I_nom + I_aux, B] int8: winning alpha position per iteration, -1 not run; + with costs every
+        line-search candidate's cost [B, I_nom + I_aux, 8] by alpha position, NaN not run)."""
         B = st["b"].shape[0]
         theta = self._a(theta)
         ws = None if w is None else np.ascontiguousarray(self._a(w).T)
@@ -213,16 +220,20 @@ class Oracle:
         iters = np.zeros((2, B), np.int32)
         for k in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux"):
             assert st[k].dtype == self.dt and st[k].flags.c_contiguous, k
-        ch = (np.full((max(tcfg.nom_ilqr.max_iter + tcfg.aux_ilqr.max_iter, 1), B), -1, np.int8)
-              if choices else None)
+        NI = tcfg.nom_ilqr.max_iter + tcfg.aux_ilqr.max_iter
+        ch = np.full((max(NI, 1), B), -1, np.int8) if choices else None
+        cc = np.full((max(NI, 1), 8, B), np.nan, self.dt) if costs else None
         self._f("oracle_tube_step_ex")(C.byref(spec), C.byref(tcfg), C.c_longlong(B), C.c_longlong(goff),
                                        C.c_longlong(step), _p(st["x"]), _p(st["b"]), _p(st["xbar"]), _p(st["bbar"]),
                                        _p(st["Xnom"]), _p(st["Unom"]), _p(st["Xaux"]), _p(st["Uaux"]), _p(theta),
-                                       _p(ws), _p(gout), _p(log), _p(status), _p(iters), _p(ch),
+                                       _p(ws), _p(gout), _p(log), _p(status), _p(iters), _p(ch), _p(cc),
                                        C.c_int(self.nthreads))
+        out = (gout, log, status, iters)
         if choices:
-            return gout, log, status, iters, ch[:tcfg.nom_ilqr.max_iter + tcfg.aux_ilqr.max_iter]
-        return gout, log, status, iters
+            out = out + (ch[:NI],)
+        if costs:
+            out = out + (np.ascontiguousarray(np.transpose(cc[:NI], (2, 0, 1))),)
+        return out
 
     def theta_update(self, adapt, inv_batch, sums, theta, vel):
         sums, theta, vel = self._a(sums), self._a(theta).copy(), self._a(vel).copy()

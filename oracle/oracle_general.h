@@ -188,14 +188,14 @@ static int FN(general1)(const SPEC_T* s0, const dtmpc_general_cfg* cfg, const GP
   REAL* wk2 = dln + 4 * (N + 1);    /* sens1 scratch */
   int st = 0;
   REAL x0[4] = {xb[0], xb[1], xb[2], bb};
-  st |= FN(ilqr1)(&sn, &cn, &cfg->nom_ilqr, x0, NULL, NULL, Xn, Vn, K, kf, itn, wk, NULL, 0);
+  st |= FN(ilqr1)(&sn, &cn, &cfg->nom_ilqr, x0, NULL, NULL, Xn, Vn, K, kf, itn, wk, NULL, 0, NULL);
   for (int k = 0; k <= N; ++k)
     for (int f = 0; f < 3; ++f) Xr[3 * k + f] = Xn[4 * k + f];
   x0[0] = xs[0];
   x0[1] = xs[1];
   x0[2] = xs[2];
   x0[3] = bs;
-  st |= FN(ilqr1)(&sa, &ca, &cfg->aux_ilqr, x0, Xr, Vn, Xa, Va, K, kf, ita, wk, NULL, 0);
+  st |= FN(ilqr1)(&sa, &ca, &cfg->aux_ilqr, x0, Xr, Vn, Xa, Va, K, kf, ita, wk, NULL, 0, NULL);
   /* upper loss L = ||x* - xbar||^2 + ||b*||^2 (:403-408) */
   REAL L1 = 0, L2 = 0;
   for (int k = 0; k <= N; ++k) {
@@ -547,7 +547,7 @@ void FN(oracle_nominal_receding)(const dtmpc_spec* sp, const dtmpc_cost* cp, con
       for (int t = 0; t < H; ++t) {
         int it = 0;
         REAL x0h[4] = {xh[0], xh[1], xh[2], xh[3]};
-        st |= FN(ilqr1)(&s, &c, cfg, x0h, NULL, NULL, X, V, K, kf, &it, wk, NULL, 0);
+        st |= FN(ilqr1)(&s, &c, cfg, x0h, NULL, NULL, X, V, K, kf, &it, wk, NULL, 0, NULL);
         REAL u0[2] = {V[0], V[1]}, xn[4];
         FN(fhat)(&s, xh, u0, xn);
         REAL rec[6] = {xh[0], xh[1], xh[2], u0[0], u0[1], xh[3]};

@@ -462,10 +462,12 @@ static REAL FN(traj_cost)(const SPEC_T* s, const COST_T* c, const REAL* X, const
 
 /* work: >= (2*(N+1)*4 + 2*2*N) REALs. Returns status bits; *iters = iterations run.  choice (or NULL):
  * the line search's winning alpha position of iteration it at choice[it * cstride] (the decision record
- * of SURVEY.md §8c; iterations not run are left as the caller set them). */
+ * of SURVEY.md §8c; iterations not run are left as the caller set them).  ccost (or NULL): the cost of
+ * every line-search candidate, alpha position ia of iteration it at ccost[(it * 8 + ia) * cstride] (the
+ * candidates' costs behind each decision: the tie-aware decision gate of tests/_common.py). */
 static int FN(ilqr1)(const SPEC_T* s, const COST_T* c, const dtmpc_ilqr_cfg* cfg, const REAL* x0,
                      const REAL* Xr, const REAL* Ur, REAL* X, REAL* V, REAL* K, REAL* kff,
-                     int* iters, REAL* work, signed char* choice, long long cstride) {
+                     int* iters, REAL* work, signed char* choice, long long cstride, REAL* ccost) {
   int N = s->N;
   REAL reg = (REAL)cfg->reg, tol = (REAL)cfg->tol;
   REAL* Xc = work;
@@ -542,6 +544,7 @@ static int FN(ilqr1)(const SPEC_T* s, const COST_T* c, const dtmpc_ilqr_cfg* cfg
       for (int j = 0; j < 2 * N; ++j)
         if (!FN(isfin)(Vc[j])) return DTMPC_ST_NONFINITE;
       REAL J = FN(traj_cost)(s, c, Xc, Vc, Xr, Ur);
+      if (ccost && ia < 8) ccost[((long long)it * 8 + ia) * cstride] = J;
       if (!FN(isfin)(J)) return DTMPC_ST_NONFINITE;
       if (!have_best || J < best) {
         have_best = 1;
@@ -873,11 +876,12 @@ void FN(oracle_linearize)(const dtmpc_spec* sp, const dtmpc_cost* cp, long long 
   }
 }
 
-/* choices (or NULL): [max_iter][B] winning alpha position per iteration, -1 where none ran */
+/* choices (or NULL): [max_iter][B] winning alpha position per iteration, -1 where none ran;
+ * costs (or NULL): [max_iter][8][B] every line-search candidate's cost by alpha position (NaN: not run) */
 void FN(oracle_ilqr_solve_ex)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cfg,
                               long long B, const REAL* x0, const REAL* Xref, const REAL* Uref,
                               REAL* X, REAL* U, REAL* K, REAL* kff, int* iters, int* status,
-                              signed char* choices, int nthreads) {
+                              signed char* choices, REAL* costs, int nthreads) {
   SPEC_T s;
   COST_T c;
   FN(spec_from)(sp, &s);
@@ -910,9 +914,11 @@ void FN(oracle_ilqr_solve_ex)(const dtmpc_spec* sp, const dtmpc_cost* cp, const 
       int it = 0;
       if (choices)
         for (int j = 0; j < cfg->max_iter; ++j) choices[(long long)j * B + i] = -1;
+      if (costs)
+        for (int j = 0; j < cfg->max_iter * 8; ++j) costs[(long long)j * B + i] = (REAL)NAN;
       int st = FN(ilqr1)(&s, &c, cfg, x0a, c.kind == DTMPC_COST_TRACK ? Xr : NULL,
                          c.kind == DTMPC_COST_TRACK ? Ur : NULL, Xa, Va, Ka, ka, &it, wk,
-                         choices ? choices + i : NULL, B);
+                         choices ? choices + i : NULL, B, costs ? costs + i : NULL);
       FN(scatter)(Xa, N + 1, 4, B, i, X);
       FN(scatter)(Va, N, 2, B, i, U);
       if (K) FN(scatter)(Ka, N, 8, B, i, K);
@@ -989,12 +995,13 @@ void FN(oracle_doc_grad)(int N, long long B, const REAL* Xa, const REAL* Ua, con
  * State arrays SoA as dtmpc_tube_state (host memory).  gout [7][B] per-trajectory L, gQ, gR, gqb.
  * log [18][B] (may be NULL).  w [3][B] (may be NULL when cfg->disturbance == 1). */
 /* choices (or NULL): [nom max_iter + aux max_iter][B] winning alpha position per iteration of the
- * nominal, then the ancillary solve, -1 where none ran */
+ * nominal, then the ancillary solve, -1 where none ran; costs (or NULL): [nom + aux max_iter][8][B] the
+ * candidates' costs of every line search by alpha position (NaN: not run) */
 void FN(oracle_tube_step_ex)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long long B,
                              long long goff, long long step, REAL* x, REAL* b, REAL* xbar,
                              REAL* bbar, REAL* Xnom, REAL* Unom, REAL* Xaux, REAL* Uaux,
                              const REAL* theta, const REAL* w, REAL* gout, REAL* log, int* status,
-                             int* iters, signed char* choices, int nthreads) {
+                             int* iters, signed char* choices, REAL* costs, int nthreads) {
   SPEC_T s;
   COST_T cn, ca;
   FN(spec_from)(sp, &s);
@@ -1042,15 +1049,19 @@ void FN(oracle_tube_step_ex)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, lo
       FN(gather)(Unom, N, 2, B, i, Vn);
       if (choices)
         for (int j = 0; j < cfg->nom_ilqr.max_iter + cfg->aux_ilqr.max_iter; ++j) choices[(long long)j * B + i] = -1;
+      if (costs)
+        for (int j = 0; j < (cfg->nom_ilqr.max_iter + cfg->aux_ilqr.max_iter) * 8; ++j)
+          costs[(long long)j * B + i] = (REAL)NAN;
       st |= FN(ilqr1)(&s, &cn, &cfg->nom_ilqr, x0, NULL, NULL, Xn, Vn, Ka, ka, &itn, wk,
-                      choices ? choices + i : NULL, B);
+                      choices ? choices + i : NULL, B, costs ? costs + i : NULL);
       /* ancillary solve tracking the nominal :863-909 */
       for (int k = 0; k <= N; ++k)
         for (int f = 0; f < 3; ++f) Xr[3 * k + f] = Xn[4 * k + f];
       x0[0] = xs[0]; x0[1] = xs[1]; x0[2] = xs[2]; x0[3] = bs;
       FN(gather)(Uaux, N, 2, B, i, Va);
       st |= FN(ilqr1)(&s, &ca, &cfg->aux_ilqr, x0, Xr, Vn, Xa, Va, Ka, ka, &ita, wk,
-                      choices ? choices + (long long)cfg->nom_ilqr.max_iter * B + i : NULL, B);
+                      choices ? choices + (long long)cfg->nom_ilqr.max_iter * B + i : NULL, B,
+                      costs ? costs + (long long)cfg->nom_ilqr.max_iter * 8 * B + i : NULL);
       /* sensitivity + DOC gradient :915-976 */
       st |= FN(sens1)(&s, &ca, Xa, Va, Xr, Vn, Xr, NULL, NULL, dXa, dVa, NULL, wk2);
       REAL o[7];
@@ -1110,14 +1121,14 @@ void FN(oracle_tube_step)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cfg, long 
                           const REAL* theta, const REAL* w, REAL* gout, REAL* log, int* status,
                           int* iters, int nthreads) {
   FN(oracle_tube_step_ex)(sp, cfg, B, goff, step, x, b, xbar, bbar, Xnom, Unom, Xaux, Uaux, theta, w, gout, log,
-                          status, iters, NULL, nthreads);
+                          status, iters, NULL, NULL, nthreads);
 }
 
 void FN(oracle_ilqr_solve)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cfg,
                            long long B, const REAL* x0, const REAL* Xref, const REAL* Uref,
                            REAL* X, REAL* U, REAL* K, REAL* kff, int* iters, int* status,
                            int nthreads) {
-  FN(oracle_ilqr_solve_ex)(sp, cp, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, NULL, nthreads);
+  FN(oracle_ilqr_solve_ex)(sp, cp, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, NULL, NULL, nthreads);
 }
 
 /* momentum + projected update core/tube_mpc.py:978-984 with g = sums[1:7] * inv_batch, or for

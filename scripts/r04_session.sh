@@ -1,0 +1,42 @@
+#!/usr/bin/env bash
+# Round-4 GPU session (one gpurun call): smoke, the whole -m gpu suite with the parity prints (-s), then a
+# short default bench line.  Every GPU step runs under its own time limit; a crash / timeout / abort ends
+# the session (pytest assertion failures, exit 1, do not).  Logs: gpurun_out/r04_<TAG>/.
+# usage: bash scripts/r04_session.sh TAG [steps: smoke tests bench] [pytest -k expression]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-s1}
+STEPS=${2:-"smoke tests bench"}
+KEXPR=${3:-}
+OUT=gpurun_out/r04_$TAG
+mkdir -p "$OUT"
+run() {  # name seconds cmd...
+  local name=$1 secs=$2
+  shift 2
+  echo "[r04] $name: $*" | tee -a "$OUT/session.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[r04] $name rc=$rc" | tee -a "$OUT/session.log"
+  tail -n 4 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "[r04] stopping after $name (rc=$rc)" | tee -a "$OUT/session.log"
+    exit $rc
+  fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests)
+      if [ -n "$KEXPR" ]; then
+        run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf -s --timeout 300 --timeout-method thread -k "$KEXPR"
+      else
+        run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf -s --timeout 300 --timeout-method thread
+      fi ;;
+    bench) run bench 900 python bench.py --steps 10 --warmup 3 ;;
+    bench_quick) run bench_quick 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-steady ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+grep -h "^\[f32 vs f64\|^\[tie-aware\|^\[decisions" "$OUT/pytest_gpu.log" > "$OUT/parity_lines.txt" 2>/dev/null
+exit 0

@@ -122,3 +122,130 @@ def decision_agreement(dev_ch, oracle_chs, dev_U=None, oracle_Us=None, label: st
     for i in bad[:show]:
         print(f"    traj {i}: device {dev_ch[i].tolist()} oracle {chs[0][i].tolist()}")
     return res
+
+
+# --------------------------------------------------------------------------------------------------------
+# f32 against f64 truth, and the tie-aware decision gate (VERDICT r03 "next" #1)
+def f64_truth(dev_out, build_outs, truth, k: float = 1.5, floor: float = 2e-5):
+    """Per trajectory: the device's f32 error against the f64 oracle (the truth: the reference's configured
+    precision, configs/dubins.yaml:8) must be no worse than k x the worst f32 oracle build's error against
+    the same truth (floor: below it every f32 evaluation is at rounding level -- a ratio of two rounding
+    noises says nothing).  Also the fraction within SURVEY.md §8c's 1e-3 for the device and every build.
+    Returns dict(frac_ok, e_dev, e_worst, within_1e3_dev, within_1e3_builds)."""
+    e_dev = rel_rows(dev_out, truth)
+    e_b = np.stack([rel_rows(o, truth) for o in build_outs])
+    worst = e_b.max(0)
+    ok = e_dev <= np.maximum(k * worst, floor)
+    return {"frac_ok": float(ok.mean()), "e_dev": e_dev, "e_worst": worst,
+            "within_1e3_dev": float((e_dev <= 1e-3).mean()),
+            "within_1e3_builds": [float((e <= 1e-3).mean()) for e in e_b],
+            "bad": np.nonzero(~ok)[0].tolist()}
+
+
+def _ulp32(J):
+    return np.spacing(np.abs(np.asarray(J, np.float32))).astype(np.float64)
+
+
+def _first_split(ca, cb):
+    """First iteration where two decision sequences differ (-1: none)."""
+    d = np.nonzero(ca != cb)[0]
+    return int(d[0]) if d.size else -1
+
+
+def _split_margin(chA, JA, chB, JB, t, tol, t0=0):
+    """At the first split t of evaluation A (device) against evaluation B (an oracle build), the margin by
+    which B's own costs separate the two choices, in ulps of B's winning cost, and the cost drift between
+    A and B before the split (the previous winner's cost in both, or the alpha = 0 candidate -- the
+    initial tape -- at t = 0), in the same ulps.
+    An iteration-count split (one ran iteration t, the other stopped: the tol exit, core/ddp.py:303) is
+    measured on the exit test instead: | |J_prev - J_best| - tol | of the run that went on."""
+    ca, cb = int(chA[t]), int(chB[t])
+    if ca >= 0 and cb >= 0:
+        jb = JB[t]
+        win = float(jb[cb])
+        u = float(_ulp32(win))
+        margin = abs(float(jb[ca]) - win) / u if np.isfinite(jb[ca]) else np.inf
+        kind = "alpha"
+    else:  # exit split: the run that continued had |prev - best| >= tol at iteration t - 1
+        run, ch = (JB, chB) if cb >= 0 else (JA, chA)
+        if t - t0 < 2:
+            return "exit", np.inf, 0.0
+        prev, best = float(run[t - 2][ch[t - 2]]), float(run[t - 1][ch[t - 1]])
+        u = float(_ulp32(best))
+        margin = abs(abs(prev - best) - tol) / u
+        kind = "exit"
+    if t == t0:  # first iteration of a solve: the initial tapes' drift, on the alpha = 0 candidate
+        z = np.nonzero(np.isfinite(JA[t]) & np.isfinite(JB[t]))[0]
+        drift = float(np.min(np.abs(JA[t][z] - JB[t][z]))) / u if z.size else np.inf
+    else:
+        p = int(chB[t - 1])
+        drift = abs(float(JA[t - 1][p]) - float(JB[t - 1][p])) / u
+    return kind, margin, drift
+
+
+def tie_aware_decisions(dev_ch, dev_costs, chs, costs, tol: float = -1.0, ulps: float = 8.0, k_drift: float = 4.0,
+                        label: str = "", show: int = 6, starts=(0,)):
+    """Tie-aware decision gate (SURVEY.md §8c decision agreement).
+
+    dev_ch / chs: [B, I] winning alpha positions of the device and of each oracle build (-1 not run);
+    dev_costs / costs: [B, I, 8] every candidate's cost by alpha position.  A trajectory passes when its
+    decision sequence equals some build's, or when at its first split from a build the split is a
+    near-tie: that build's own costs separate the two choices by at most max(ulps, k_drift x drift) ulps
+    of the winning cost, drift being how far the device's and the build's costs had already moved apart
+    on the same candidate before the split (ulps: a tie at fp32 resolution of the cost sum; k_drift x
+    drift: the rounding carried in from earlier iterations of a chaotic recursion).  Exit splits (the
+    tol test) are held to the same bound on | |J_prev - J_best| - tol |.  The same statistic between the
+    builds themselves is printed as the calibration: a device whose splits look like the builds' mutual
+    splits is a fourth valid rounding of the same algorithm.  starts: the first record index of each
+    solve in the sequence (the tube step: nominal then ancillary iterations)."""
+    t0_of = lambda t: max(s_ for s_ in starts if s_ <= t)  # noqa: E731
+    dev_ch, dev_costs = np.asarray(dev_ch), np.asarray(dev_costs, np.float64)
+    chs = [np.asarray(c) for c in chs]
+    costs = [np.asarray(c, np.float64) for c in costs]
+    B = dev_ch.shape[0]
+    res = {"n": int(B), "exact": 0, "tie": 0, "fail": [], "margins": [], "drifts": []}
+
+    def best_split(cA, JA, i):
+        out = None
+        for cB, JB in zip(chs, costs):
+            t = _first_split(cA[i], cB[i])
+            if t < 0:
+                return "exact", 0.0, 0.0, -1
+            kind, m, d = _split_margin(cA[i], JA[i], cB[i], JB[i], t, tol, t0_of(t))
+            allowed = max(ulps, k_drift * d)
+            score = m / allowed
+            if out is None or score < out[0]:
+                out = (score, kind, m, d, t)
+        return out[1], out[2], out[3], out[4]
+
+    for i in range(B):
+        kind, m, d, t = best_split(dev_ch, dev_costs, i)
+        if kind == "exact":
+            res["exact"] += 1
+            continue
+        res["margins"].append(m)
+        res["drifts"].append(d)
+        if m <= max(ulps, k_drift * d):
+            res["tie"] += 1
+        else:
+            res["fail"].append((i, kind, t, m, d))
+    res["frac_ok"] = (res["exact"] + res["tie"]) / B
+    # calibration: build 1 and 2 against build 0 (the same measurement between valid roundings)
+    cal = []
+    for cB, JB in zip(chs[1:], costs[1:]):
+        for i in range(B):
+            t = _first_split(cB[i], chs[0][i])
+            if t >= 0:
+                cal.append(_split_margin(cB[i], JB[i], chs[0][i], costs[0][i], t, tol, t0_of(t))[1])
+    mg = np.asarray(res["margins"]) if res["margins"] else np.zeros(0)
+    cm = np.asarray(cal) if cal else np.zeros(0)
+    q = lambda a, p: float(np.quantile(a[np.isfinite(a)], p)) if np.isfinite(a).any() else float("nan")  # noqa: E731
+    res["margin_ulps_median"], res["margin_ulps_p90"] = q(mg, 0.5), q(mg, 0.9)
+    res["builds_margin_ulps_median"], res["builds_margin_ulps_p90"] = q(cm, 0.5), q(cm, 0.9)
+    print(f"[tie-aware decisions{(' ' + label) if label else ''}] B={B}: exact {res['exact']}, near-tie splits "
+          f"{res['tie']}, failing {len(res['fail'])} -> {res['frac_ok']:.4f}; split margins (ulp of J) median "
+          f"{res['margin_ulps_median']:.3g} p90 {res['margin_ulps_p90']:.3g}; builds among themselves median "
+          f"{res['builds_margin_ulps_median']:.3g} p90 {res['builds_margin_ulps_p90']:.3g}")
+    for f in res["fail"][:show]:
+        print(f"    traj {f[0]}: {f[1]} split at iteration {f[2]}, margin {f[3]:.3g} ulp, drift {f[4]:.3g} ulp")
+    return res

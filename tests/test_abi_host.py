@@ -177,10 +177,10 @@ def test_arguments_validated_before_any_device_call(lib):
     assert lib.dtmpc_ilqr_workspace_bytes(_abi.F64, 50, 4096, 4) == 2 * ip4 * 4096
     assert lib.dtmpc_ilqr_workspace_bytes(_abi.F64, 50, 65536, 0) == 2 * ip1 * 65536
     rc = lib.dtmpc_ilqr_solve_ws(_abi.F32, C.byref(spec), C.byref(cost), C.byref(st.ilqr_nom.to_c()), 4, 1, None, None,
-                                 1, 1, 1, 1, None, 1, None, 3, None, 0, None)
+                                 1, 1, 1, 1, None, 1, None, None, 3, None, 0, None)
     assert rc == _abi.ERR_BAD_ARG and b"lanes" in lib.dtmpc_last_error()
     rc = lib.dtmpc_ilqr_solve_ws(_abi.F32, C.byref(spec), C.byref(cost), C.byref(st.ilqr_nom.to_c()), 4, 1, None, None,
-                                 1, 1, 1, 1, None, 1, None, 4, None, 100, None)
+                                 1, 1, 1, 1, None, 1, None, None, 4, None, 100, None)
     assert rc == _abi.ERR_BAD_ARG and b"work_bytes" in lib.dtmpc_last_error()
     # the fused episode reset validates before launching
     rc = lib.dtmpc_tube_reset(_abi.F32, C.byref(spec), 8, None, C.byref(state), 1, 1, 1, None)

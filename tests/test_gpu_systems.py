@@ -212,3 +212,68 @@ def test_cost_derivs_u_form(dev, tag):
         assert torch.equal(pxx.cpu()[..., 3, 3], torch.zeros_like(pxx.cpu()[..., 3, 3]))
         px, _ = CD.auxiliary_terminal_derivs(x_hat_N=D(sel(xh)), x_ref_N=D(sel(xr)), Qf=Qf)
         assert torch.equal(px.cpu(), torch.cat([2.0 * Qf * (x[..., :3] - sel(xr)), torch.zeros_like(x[..., :1])], -1))
+
+
+@pytest.mark.parametrize("setting", ["s0", "s1"])
+def test_autograd_through_per_function_api(dev, setting):
+    """the reference differentiates its per-function API with autograd
+    (core/ddp.py:63-86 _linearize_autograd, core/autodiff.py:9-80).  Here dubins_step, h_*, the barriers and
+    BoxClampControl.clamp are autograd Functions whose backward is the library's analytic derivative, so the
+    autograd Jacobian of the reference's DBaS closure f_hat(x_hat, u) = [f(x, u), dbas_step b'] equals
+    dubins_augmented_jacobian (inverse barrier: the reference's f_jac), dubins_step's Jacobian dubins_f_jac,
+    and a second derivative of dubins_step exists.  The entry points with no autograd formula raise instead
+    of returning an output cut from the graph."""
+    from diff_tube_mpc_strict_pt.core.barrier import DBaSConfig, dbas_step
+    from diff_tube_mpc_strict_pt.core.control import BoxClampControl
+    from diff_tube_mpc_strict_pt.core.cost_derivs import nominal_cost_derivs_u
+    from diff_tube_mpc_strict_pt.core.systems import dubins_obstacles as O
+    from diff_tube_mpc_strict_pt.core.systems.dubins import dubins_step
+    from diff_tube_mpc_strict_pt.core.systems.dubins_aug_jac import dubins_augmented_jacobian, dubins_f_jac
+
+    tdt = torch.float64
+    k = golden("kat_f64")
+    dub, obs, beta, eps = _setup()
+    st = SETTINGS[setting]
+    dbc = DBaSConfig(barrier_type="inverse", alpha=st["alpha"], gamma=st["gamma"], eps=eps)
+    if st["agg"] == "smoothmin":
+        h = lambda x: O.h_multi_circle_obstacles(x, obstacles=obs, beta=beta)  # noqa: E731
+    else:
+        h = lambda x: O.h_min_circle_obstacles(x, obstacles=obs)  # noqa: E731
+    f = lambda x, u: dubins_step(x, u, cfg=dub)  # noqa: E731
+
+    def fhat(xh, u):
+        xn, bn = dbas_step(x_k=xh[:3], u_k=u, b_k=xh[3], f=f, h=h, cfg=dbc)
+        return torch.cat([xn, bn.reshape(1)])
+
+    xh_all = torch.tensor(k["xh"], dtype=tdt, device=dev)
+    u_all = torch.tensor(k["u"], dtype=tdt, device=dev)
+    for i in range(0, 96, 12):
+        xh, u = xh_all[i], u_all[i]
+        Aa, Ba = torch.autograd.functional.jacobian(fhat, (xh, u))
+        A, Bm = dubins_augmented_jacobian(xh, u, cfg=dub, obs=obs, db_cfg=dbc, obs_beta=beta, obs_agg=st["agg"])
+        scale = max(1.0, float(A.abs().max()), float(Bm.abs().max()))
+        assert float((Aa - A).abs().max()) <= 1e-10 * scale, (i, Aa, A)
+        assert float((Ba - Bm).abs().max()) <= 1e-10 * scale, (i, Ba, Bm)
+        Ja, Jb = torch.autograd.functional.jacobian(lambda x, v: f(x, v), (xh[:3], u))
+        A3, B3 = dubins_f_jac(xh[:3], u, cfg=dub)
+        assert torch.allclose(Ja, A3, rtol=0, atol=1e-14) and torch.allclose(Jb, B3, rtol=0, atol=1e-14)
+    # a second derivative through dubins_step (autodiff.grad_hess_xu differentiates twice)
+    x = xh_all[0, :3].clone().requires_grad_(True)
+    u = u_all[0].clone().requires_grad_(True)
+    (gx,) = torch.autograd.grad(f(x, u)[0], x, create_graph=True)
+    (hxx,) = torch.autograd.grad(gx[2], x)
+    ref = -dub.dt * float(u[0]) * math.cos(float(x[2]))  # d2 px' / dtheta2
+    assert abs(float(hxx[2]) - ref) <= 1e-14
+    # clamp: torch.clamp's gradient rule
+    box = BoxClampControl(u_min=(-10.0, -math.pi), u_max=(10.0, math.pi))
+    uu = torch.tensor([[-12.0, 0.5], [10.0, 4.0], [3.0, -math.pi]], dtype=tdt, device=dev, requires_grad=True)
+    box.clamp(uu).sum().backward()
+    assert uu.grad.cpu().tolist() == [[0.0, 1.0], [1.0, 0.0], [1.0, 1.0]]
+    # no autograd formula: refuse rather than detach silently
+    xg = xh_all[:4].clone().requires_grad_(True)
+    with pytest.raises(RuntimeError, match="autograd"):
+        dubins_augmented_jacobian(xg, u_all[:4], cfg=dub, obs=obs, db_cfg=dbc, obs_beta=beta, obs_agg=st["agg"])
+    with pytest.raises(RuntimeError, match="autograd"):
+        nominal_cost_derivs_u(x_hat=xg, u=u_all[:4], target=(10.0, 10.0, 0.7), Q=(1.0, 1.0, 1.0), R=(1.0, 1.0), qb=1.0)
+    with torch.no_grad():  # detached use stays allowed
+        dubins_augmented_jacobian(xg, u_all[:4], cfg=dub, obs=obs, db_cfg=dbc, obs_beta=beta, obs_agg=st["agg"])
