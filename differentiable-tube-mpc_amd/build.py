@@ -57,12 +57,17 @@ def _key(cmd, src) -> str:
     return h.hexdigest()[:24]
 
 
-def build(force: bool = False, variant: str = "", defines=(), only=()) -> str:
+PRODUCT_OBJS = os.path.join(CACHE, "product_objs.txt")  # the product library's objects, one per line
+
+
+def build(force: bool = False, variant: str = "", defines=(), only=(), on_product: bool = False) -> str:
     """Build the library.  ``variant`` (with extra ``-D`` defines) writes libdtmpc_<variant>.so next to
     the product library, for A/B kernel experiments loaded through DTMPC_LIBRARY; it never replaces
     libdtmpc.so.  ``only`` restricts the defines / extra flags to the named translation units (e.g.
     ``dtmpc_fast``); objects are cached under build/obj by command line and source text, so a variant
-    recompiles only the units its flags reach."""
+    recompiles only the units its flags reach.  ``on_product`` (variants with ``only``): the units not named
+    are taken from the last product build as they are (build/obj/product_objs.txt), never recompiled -- an A/B
+    of one unit against exactly the product library's other objects."""
     out = OUT if not variant else OUT.replace("libdtmpc.so", f"libdtmpc_{variant}.so")
     if not variant and not force and up_to_date():
         return out
@@ -70,9 +75,18 @@ def build(force: bool = False, variant: str = "", defines=(), only=()) -> str:
     os.makedirs(CACHE, exist_ok=True)
     objs = []
     procs = []
+    prod = {}
+    if on_product:
+        if not variant or not only:
+            raise ValueError("on_product needs a variant and the units it rebuilds (only)")
+        for o in open(PRODUCT_OBJS).read().split():
+            prod[os.path.basename(o).split(".")[0]] = o
     for src in SRCS:
         tu = os.path.splitext(os.path.basename(src))[0]
         reach = not only or tu in only
+        if on_product and not reach:
+            objs.append(prod[tu])
+            continue
         extra = os.environ.get("DTMPC_EXTRA_FLAGS", "").split() if variant and reach else []
         defs = [f"-D{d}" for d in defines] if reach else []
         cmd = [HIPCC, *FLAGS, *extra, *defs, "-c"]
@@ -94,6 +108,8 @@ def build(force: bool = False, variant: str = "", defines=(), only=()) -> str:
     if key is not None:
         with open(out + ".key", "w") as f:
             f.write(key)
+        with open(PRODUCT_OBJS, "w") as f:
+            f.write("\n".join(objs) + "\n")
     return out
 
 
@@ -105,5 +121,7 @@ if __name__ == "__main__":
     ap.add_argument("--variant", default="")
     ap.add_argument("-D", dest="defines", action="append", default=[])
     ap.add_argument("--only", action="append", default=[], help="translation unit(s) the -D / extra flags reach")
+    ap.add_argument("--on-product", action="store_true",
+                    help="with --variant/--only: link the other units from the last product build as they are")
     a = ap.parse_args()
-    print(build(force=a.force, variant=a.variant, defines=a.defines, only=tuple(a.only)))
+    print(build(force=a.force, variant=a.variant, defines=a.defines, only=tuple(a.only), on_product=a.on_product))

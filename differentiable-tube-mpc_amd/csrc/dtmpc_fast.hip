@@ -82,10 +82,14 @@ struct FP {
 // nominal MPC; barrier_dyn(s, h - s.tight) in the generic kernels).  Instantiations without the flag are
 // the tube step's and carry no extra instruction.
 constexpr int kTight = 16;
+// kWrap: the nominal target cost with the heading error wrapped to (-pi, pi] (run_nominal.py:297-324, the
+// receding-horizon driver's stage / terminal cost and derivatives); only the receding kernel sets it.
+constexpr int kWrap = 32;
 template <int M>
 struct Obs {
   static constexpr int n = M & (kTight - 1);
   static constexpr bool tight = (M & kTight) != 0;
+  static constexpr bool wrap = (M & kWrap) != 0;
 };
 
 struct FCost {  // nominal: target; ancillary: tracking (terminal weight = stage weight)
@@ -257,80 +261,29 @@ __device__ __forceinline__ void rst2(Rsrc, const RA& a, int k, unsigned off, f2 
 }
 #endif
 
-// LDS-resident gains (compile-time option, OFF by default: -D DTMPC_FAST_LDS_STEPS=n keeps the iLQR gains
-// of the first n steps in the LDS of the trajectory's CU instead of the workspace).  The backward pass
-// would write them there and the line search and the commit read them (core/ddp.py:248-249, 266-269):
-// three HBM passes over 32 B per step and iteration that never leave the CU.  Layout: one workgroup per
-// CU holds all 160 KiB; quad q (16 B) of step s of the trajectory with workgroup-local index j is at
-// lds[(s * Q + q) * LS + j] (LS = trajectories per workgroup), a wave's access 64 consecutive 16-B slots
-// (conflict-free ds_read/write_b128), the lanes of one trajectory reading one address (broadcast).
-// Measured and rejected (round 3, same-box A/B, profiles/r03/ab_lds.txt): 20 steps at one lane per
-// trajectory 4.05 -> 4.12 ms at B = 65,536, the whole horizon at four lanes 2.21 -> 2.52 ms at B = 4,096
-// -- the step is issue- and latency-bound, not HBM-bound, and a ds_write_b128 costs a wave ~13-26 issue
-// cycles against a buffer store's few; the bytes saved do not buy time.
-typedef __attribute__((address_space(3))) f4 lf4;
-constexpr int kLdsF4 = 163840 / (int)sizeof(f4);  // 160 KiB: the whole LDS of a CU, one workgroup per CU
-
-template <int P, bool G0>
-struct GainLds {
-  static constexpr int Q = G0 ? 2 : 3;          // 16-byte quads per step: K (2) [+ k]
-  static constexpr int LS = kBlock / P;         // trajectories per workgroup
-  // steps held in LDS (at most what fits).  Only the gamma = 0 records: with the general 40-byte records
-  // in three quads per step the results differed from the workspace-only path in a same-box diagnostic
-  // (scripts/diag_g0.py; deterministic, cause not found), so those always stay in the workspace.
-#ifndef DTMPC_FAST_LDS_STEPS
-#define DTMPC_FAST_LDS_STEPS 0
-#endif
-#ifndef DTMPC_FAST_LDS_GENERAL
-#define DTMPC_FAST_LDS_GENERAL 0  // 1: the general 40-byte records in LDS too (round-4 root-cause experiment)
-#endif
-  static constexpr int KL = ((!G0 && !DTMPC_FAST_LDS_GENERAL) || DTMPC_FAST_F64) ? 0 : kLdsF4 / (LS * Q) < DTMPC_FAST_LDS_STEPS ? kLdsF4 / (LS * Q) : DTMPC_FAST_LDS_STEPS;
-  static constexpr bool used = KL > 0;
-};
+// (LDS-resident gains -- the first steps' iLQR gains kept in the CU's LDS instead of the workspace -- were
+// built in round 3, measured slower at every lane form (profiles/r03/ab_lds.txt) and deleted in round 4: with
+// the option off, the step-index test in front of every gain access was still compiled as a runtime branch
+// (the sign of a readfirstlane'd index is unknown to the compiler))
 
 template <int P>
 struct Gains {
-  RA K, k;     // K and k records (the steps past KL, and the sensitivity pass's full records)
-  lf4* L;      // this trajectory's LDS column (lds + workgroup-local trajectory index)
-  bool w;      // this lane writes the LDS copy (the trajectory's first lane; P = 1: every lane)
+  RA K, k;     // K and k records (the iLQR's; the sensitivity pass's full records)
   // G0 (gamma = 0): K's column for the barrier state b is exactly zero (A's column 3 is (0, 0, 0, gamma),
   // so Q_ux's is gamma * S = 0 and K = -Q_uu^-1 Q_ux keeps it), and the iLQR record is the 32 bytes
   // K00 K01 K02 K10 | K11 K12 k0 k1 -- 8 B less per step, two loads instead of three
   template <bool G0>
   __device__ __forceinline__ void store(Rsrc r, int s, const real* Kk, const real* kk) const {
-    using GL = GainLds<P, G0>;
     const f4 g0 = G0 ? f4{Kk[0], Kk[1], Kk[2], Kk[4]} : f4{Kk[0], Kk[1], Kk[2], Kk[3]};
     const f4 g1 = G0 ? f4{Kk[5], Kk[6], kk[0], kk[1]} : f4{Kk[4], Kk[5], Kk[6], Kk[7]};
-    if (s < GL::KL) {
-      if (P == 1 || w) {
-        L[(s * GL::Q) * GL::LS] = g0;
-        L[(s * GL::Q + 1) * GL::LS] = g1;
-        if (!G0) L[(s * GL::Q + 2) * GL::LS] = f4{kk[0], kk[1], 0.f, 0.f};
-      }
-    } else {
-      rst4(r, K, s, 0, g0);
-      rst4(r, K, s, 16 * ES, g1);
-      if (!G0) rst2(r, k, s, 0, f2{kk[0], kk[1]});
-    }
+    rst4(r, K, s, 0, g0);
+    rst4(r, K, s, 16 * ES, g1);
+    if (!G0) rst2(r, k, s, 0, f2{kk[0], kk[1]});
   }
   // step s's gains: K rows (Ka, Kb; G0: the zero column as 0) and k
   template <bool G0>
   __device__ __forceinline__ void load(Rsrc r, int s, f4& Ka, f4& Kb, f2& kf) const {
-    using GL = GainLds<P, G0>;
-    f4 g0, g1;
-    f2 k2;
-    if (s < GL::KL) {
-      g0 = L[(s * GL::Q) * GL::LS];
-      g1 = L[(s * GL::Q + 1) * GL::LS];
-      if (!G0) {
-        const f4 g2 = L[(s * GL::Q + 2) * GL::LS];
-        k2 = f2{g2.x, g2.y};
-      }
-    } else {
-      g0 = rld4(r, K, s, 0);
-      g1 = rld4(r, K, s, 16 * ES);
-      if (!G0) k2 = rld2(r, k, s, 0);
-    }
+    const f4 g0 = rld4(r, K, s, 0), g1 = rld4(r, K, s, 16 * ES);
     if (G0) {
       Ka = f4{g0.x, g0.y, g0.z, 0.f};
       Kb = f4{g0.w, g1.x, g1.y, 0.f};
@@ -338,7 +291,7 @@ struct Gains {
     } else {
       Ka = g0;
       Kb = g1;
-      kf = k2;
+      kf = rld2(r, k, s, 0);
     }
   }
   // the sensitivity pass's full records K (32 B) + k (8 B), always in the workspace
@@ -412,10 +365,28 @@ __device__ __forceinline__ real vlog(real x) {
   return x == __builtin_inf() ? x : r;
 }
 __device__ __forceinline__ f2 vlog(f2 x) { return f2{vlog(x.x), vlog(x.y)}; }
+// A smooth-min term exp(-beta h_i - zmax) below exp(-kSmSkip) = exp(-50) = 1.9e-22 is taken as 0: se >= 1 (its
+// largest term is exp(0)), so at most eight such terms move se by < 1.6e-21, i.e. < 1e-5 ulp -- the f64 sum is
+// unchanged except on a one-in-10^5 rounding tie.  The rule is per value (the same candidate state gives the
+// same se in the line search, the commit and the start rollout); smsum skips the exp for an obstacle no lane
+// of the wave needs (a uniform branch: far obstacles -- h_i > h_min + 2.5 at beta = 20 -- are most of them).
+// f64 only: the f32 term is one v_exp_f32.
+constexpr double kSmSkip = 50.0;
+template <class V>
+__device__ __forceinline__ V smarg(const FP& p, V hi, V zmax) {
+  DTMPC_NOCONTRACT
+  return p.neg_beta * hi - zmax;
+}
+__device__ __forceinline__ real smexp(real x) { return x < -kSmSkip ? 0.0 : vexp(x); }
+__device__ __forceinline__ f2 smexp(f2 x) { return f2{smexp(x.x), smexp(x.y)}; }
+__device__ __forceinline__ bool smneed(real x) { return !(x < -kSmSkip); }  // NaN: needed (it propagates)
+__device__ __forceinline__ bool smneed(f2 x) { return smneed(x.x) || smneed(x.y); }
 template <class V>
 __device__ __forceinline__ V smterm(const FP& p, V hi, V zmax, V) {
-  DTMPC_NOCONTRACT
-  return vexp(p.neg_beta * hi - zmax);
+  const V x = smarg(p, hi, zmax);
+  V e = V(0.0);
+  if (__builtin_amdgcn_ballot_w64(smneed(x))) e = smexp(x);  // wave-uniform
+  return e;
 }
 #ifndef DTMPC_FAST_SINCOS_AB
 #define DTMPC_FAST_SINCOS_AB 1
@@ -610,7 +581,10 @@ __device__ __forceinline__ real h_grad(const FP& p, real px, real py, real& gx, 
 #pragma unroll
   for (int i = 0; i < MO; ++i) {
 #if DTMPC_FAST_F64
-    const real e = m_exp(z[i] - zmax);  // the generic kernel's h_grad (dtmpc_device.hpp)
+    // the generic kernel's h_grad (dtmpc_device.hpp), with the smooth-min's rule for negligible terms (smterm)
+    const real x = z[i] - zmax;
+    real e = 0.0;
+    if (__builtin_amdgcn_ballot_w64(smneed(x))) e = smexp(x);
 #else
     const real e = __builtin_amdgcn_exp2f(__builtin_fmaf(hh[i], p.nbl2e, -zl));
 #endif
@@ -649,9 +623,15 @@ __device__ __forceinline__ real barrier_at(const FP& p, real px, real py) {
   return vbarrier(p, h_sm<M>(p, px, py));
 }
 
+// _wrap_angle (run_nominal.py:32-34): atan2(sin e, cos e), evaluated as the generic kernels do (wrap_angle,
+// dtmpc_device.hpp)
+__device__ __forceinline__ real vwrap(real e) { return wrap_angle<real>(e); }
+__device__ __forceinline__ f2 vwrap(f2 e) { return f2{vwrap(e.x), vwrap(e.y)}; }
+
 // stage / terminal cost (stage_cost / term_cost, core/tube_mpc.py:823-842, 875-894): TRACK takes the
-// references r (state) and q (control), the nominal its fixed target
-template <bool TRACK, class V>
+// references r (state) and q (control), the nominal its fixed target (WRAP: heading error wrapped,
+// run_nominal.py:297-309)
+template <bool TRACK, bool WRAP = false, class V>
 __device__ __forceinline__ V stage(const FCost& c, V x0, V x1, V x2, V b, V u0, V u1, real r0, real r1, real r2,
                                    real q0, real q1) {
   DTMPC_NOCONTRACT
@@ -666,6 +646,7 @@ __device__ __forceinline__ V stage(const FCost& c, V x0, V x1, V x2, V b, V u0, 
     d0 = x0 - c.tg.x;
     d1 = x1 - c.tg.y;
     d2 = x2 - c.tg.z;
+    if (WRAP) d2 = vwrap(d2);
     e0 = u0;
     e1 = u1;
   }
@@ -673,7 +654,7 @@ __device__ __forceinline__ V stage(const FCost& c, V x0, V x1, V x2, V b, V u0, 
   const V sr = ffma(c.R1 * e1, e1, (c.R0 * e0) * e0);
   return ffma(V(c.qb), b * b, sq + sr);
 }
-template <bool TRACK, class V>
+template <bool TRACK, bool WRAP = false, class V>
 __device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, real r0, real r1, real r2) {
   DTMPC_NOCONTRACT
   V d0, d1, d2;
@@ -685,6 +666,7 @@ __device__ __forceinline__ V term(const FCost& c, V x0, V x1, V x2, V b, real r0
     d0 = x0 - c.tg.x;
     d1 = x1 - c.tg.y;
     d2 = x2 - c.tg.z;
+    if (WRAP) d2 = vwrap(d2);
   }
   const V sq = ffma(c.Qf2 * d2, d2, ffma(c.Qf1 * d1, d1, (c.Qf0 * d0) * d0));
   return ffma(V(c.qb), b * b, sq);
@@ -843,14 +825,14 @@ __device__ __forceinline__ real init_tape(const FP& p, const FCost& c, const rea
     }
     const real u0 = vclamp(v0, p.umin0, p.umax0), u1 = vclamp(v1, p.umin1, p.umax1);
     S.stu(k, f2{u0, u1});
-    if (want_cost) J = J + stage<TRACK>(c, s0, s1, s2, sb, u0, u1, R.x, R.y, R.z, Q.x, Q.y);
+    if (want_cost) J = J + stage<TRACK, Obs<M>::wrap>(c, s0, s1, s2, sb, u0, u1, R.x, R.y, R.z, Q.x, Q.y);
     fhat<M, SV::g0>(p, s0, s1, s2, sb, u0, u1, Bc);
     S.stx(k + 1, f4{s0, s1, s2, sb});
   }
   if (!want_cost) return 0.f;
   f4 R = f4{0.f, 0.f, 0.f, 0.f};
   if (TRACK) R = S.xr(N);
-  return J + term<TRACK>(c, s0, s1, s2, sb, R.x, R.y, R.z);
+  return J + term<TRACK, Obs<M>::wrap>(c, s0, s1, s2, sb, R.x, R.y, R.z);
 }
 
 // sparse augmented Jacobian (make_jac, core/systems/dubins_aug_jac.py:61-139)
@@ -1105,7 +1087,8 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
   } else {
     d0 = xn0 - c.tg.x;
     d1 = xn1 - c.tg.y;
-    d2 = xn2 - c.tg.z;
+    // WRAP: phi_x against the wrapped target x - wrap(x - t) (run_nominal.py:318-324, deriv_dx)
+    d2 = Obs<M>::wrap ? xn2 - (xn2 - vwrap(xn2 - c.tg.z)) : xn2 - c.tg.z;
   }
 #if DTMPC_FAST_RICPK
   RicP R;
@@ -1152,7 +1135,7 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
     } else {
       d0 = x0 - c.tg.x;
       d1 = x1 - c.tg.y;
-      d2 = x2 - c.tg.z;
+      d2 = Obs<M>::wrap ? x2 - (x2 - vwrap(x2 - c.tg.z)) : x2 - c.tg.z;  // run_nominal.py:311-317
     }
     const real lx[4] = {lxx[0] * d0, lxx[1] * d1, lxx[2] * d2, lxx[3] * xb};
     real lu[2];
@@ -1341,7 +1324,8 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
   }
 #pragma unroll
   for (int q = 0; q < NPR; ++q)
-    C.J[q] = C.J[q] + stage<TRACK>(c, C.a0[q], C.a1[q], C.a2[q], C.ab[q], u0[q], u1[q], s.r0, s.r1, s.r2, s.q0, s.q1);
+    C.J[q] = C.J[q] + stage<TRACK, Obs<M>::wrap>(c, C.a0[q], C.a1[q], C.a2[q], C.ab[q], u0[q], u1[q], s.r0, s.r1,
+                                                  s.r2, s.q0, s.q1);
   f2 sn[NPR], cs[NPR];
   sincos_pairs<NPR>(C.a2, sn, cs);
 #pragma unroll
@@ -1370,12 +1354,30 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
     zl[q] = zmax[q] * real(1.44269504088896341);
   }
 #pragma unroll
-  for (int i = 0; i < MO; ++i)
+  for (int i = 0; i < MO; ++i) {
+#if DTMPC_FAST_F64
+    // one wave-uniform branch per obstacle for all the lane's candidates (smterm)
+    f2 x[NPR], e[NPR];
+    bool need = false;
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      x[q] = smarg(p, hi[i][q], zmax[q]);
+      need = need || smneed(x[q]);
+      e[q] = f2(0.0);
+    }
+    if (__builtin_amdgcn_ballot_w64(need))
+#pragma unroll
+      for (int q = 0; q < NPR; ++q) e[q] = smexp(x[q]);
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) se[q] = i == 0 ? e[q] : se[q] + e[q];
+#else
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
       const f2 e = smterm(p, hi[i][q], zmax[q], zl[q]);
       se[q] = i == 0 ? e : se[q] + e;  // = 0 + e_0 + ...: e_0 >= 0, so 0 + e_0 == e_0 bitwise
     }
+#endif
+  }
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
     z[q] = p.neg_inv_beta * (zmax[q] + vlog(se[q]));
@@ -1476,7 +1478,25 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   };
   f2 u0[NPR], u1[NPR];
   const int N1 = N - 1;
-  if (DTMPC_FAST_LS_DEPTH2) {
+#ifndef DTMPC_FAST_LS_LEAD4
+#define DTMPC_FAST_LS_LEAD4 0  // P = 4: step inputs in a ring of LEAD + 1 buffers refilled LEAD steps ahead (0: as P = 1)
+#endif
+  if (P == 4 && DTMPC_FAST_LS_LEAD4 > 0) {
+    constexpr int LEAD = DTMPC_FAST_LS_LEAD4 > 0 ? DTMPC_FAST_LS_LEAD4 : 1, R = LEAD + 1;
+    auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
+    StepIn Bf[R];
+#pragma unroll
+    for (int j = 0; j < LEAD; ++j) load_step<TRACK>(Bf[j], S, ix(j));
+    for (int k = 0; k < N; k += R) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        load_step<TRACK>(Bf[(j + LEAD) % R], S, ix(k + j + LEAD));
+        if (k + j >= N) break;
+        ls_step<TRACK, M, NPR, SV::g0>(p, c, Bf[j], C, u0, u1);
+        keep(k + j, u0, u1);
+      }
+    }
+  } else if (DTMPC_FAST_LS_DEPTH2) {
   // four buffers in rotation, each refilled two steps before use
   auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
   StepIn A, Bs, Cs, Ds;
@@ -1527,7 +1547,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   bool ok = true;
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
-    const f2 Jt = C.J[q] + term<TRACK>(c, C.a0[q], C.a1[q], C.a2[q], C.ab[q], r0, r1, r2);
+    const f2 Jt = C.J[q] + term<TRACK, Obs<M>::wrap>(c, C.a0[q], C.a1[q], C.a2[q], C.ab[q], r0, r1, r2);
     Jc[2 * q] = Jt.x;
     Jc[2 * q + 1] = Jt.y;
     ok = ok && vfinite(Jt);
@@ -2037,15 +2057,13 @@ __device__ __forceinline__ FP phase_p() {
 }
 
 // GM: 0 general, 1 gamma = 0 gain records, 2 gamma = 0 gain records + Riccati step (the default at gamma = 0)
-// One workgroup per CU (the LDS gains take all of it) and so one wave per SIMD at every lane count: the
-// whole 512-register budget.
+// One wave per SIMD at every lane count (amdgpu_waves_per_eu(1, 1)): the whole 512-register budget.
 template <int M, int P, int GM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 tube_fast_kernel(FK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
   (void)kk;  // read through kargs()
-  // the gains of the first steps when DTMPC_FAST_LDS_STEPS > 0 (Gains); the workgroup sums at the end
-  __shared__ f4 lds[DTMPC_FAST_LDS_STEPS > 0 ? kLdsF4 : kBlock / 64 * DTMPC_TUBE_SUMS / 4];
+  __shared__ f4 lds[kBlock / 64 * DTMPC_TUBE_SUMS / 4];  // the workgroup sums at the end
   const int B = kargs()->a.B, Bc = kargs()->a.Bc, i0 = kargs()->a.i0;
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;  // blockDim: tube_block (64 or 256)
   const int t = gl / P, h = gl % P;  // t: index in the chunk, h: lane of the trajectory
@@ -2071,8 +2089,6 @@ tube_fast_kernel(FK kk) {
     const SlotMap sm{l16, cb * (16u * ES), l8, cb * (8u * ES)};
     const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * (16u * ES) : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * (8u * ES) : l8;
     Gains<P> G;
-    G.L = (lf4*)lds + (threadIdx.x / P);
-    G.w = h == 0;
 
     int st = 0, itn = 0, ita = 0;
     real x0, x1, x2, xb, y0, y1, y2, yb;
@@ -2225,7 +2241,7 @@ tube_fast_kernel(FK kk) {
   real ws[DTMPC_TUBE_SUMS];
 #pragma unroll
   for (int j = 0; j < DTMPC_TUBE_SUMS; ++j) ws[j] = wave_sum(acc[j]);
-  __syncthreads();  // every wave is done with its LDS gains: the first 128 bytes take the wave sums
+  __syncthreads();
   real* red = (real*)lds;
   if (lane == 0)
 #pragma unroll
@@ -2302,7 +2318,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 
 ilqr_fast_kernel(IK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
   (void)kk;  // read through ikargs()
-  __shared__ f4 lds[DTMPC_FAST_LDS_STEPS > 0 ? kLdsF4 : 1];
   const IArgs& a = ikargs()->a;
   const int B = a.B, Bc = a.Bc, i0 = a.i0;
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2322,8 +2337,6 @@ ilqr_fast_kernel(IK kk) {
   S.UA = RA{a.oU, NS * cb * (8u * ES), u0lo};
   S.XRA = RA{a.oXR, cb * (16u * ES), l16};
   S.URA = RA{a.oUR, cb * (8u * ES), l8};
-  S.G.L = (lf4*)lds + (threadIdx.x / P);
-  S.G.w = h == 0;
   S.G.K = RA{a.oK, cb * (32u * ES), l32};
   S.G.k = RA{a.ok, cb * (8u * ES), l8};
   S.X = Soa<4>{(char*)a.X, 4u * bb, L};
@@ -2373,6 +2386,134 @@ ilqr_fast_kernel(IK kk) {
     if (a.iters) a.iters[i] = it;
     a.status[i] |= st;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// the receding-horizon nominal MPC (dtmpc_nominal_receding; run_nominal.py:204-415) on the fused solver: per
+// lane one trajectory's whole task horizon -- iLQR with the angle-wrapped target cost (kWrap) -> log x, u0, b
+// -> the run's exits (non-finite solve, collision: the TRUE min_i h_i <= 0, success: ||p - target|| <= r)
+// -> plant step x <- f_hat(x, u0) -> warm-start shift U <- [U[1:], U[-1]] -- as receding_kernel
+// (dtmpc_receding.hip) does with the generic solver.  One lane per trajectory: the solves of different
+// lanes stop at their own tol exits and the runs at their own exits.
+// Workspace records of one chunk: X [N+1][Bc][4], U [N][Bc][2], gains K [N][Bc][8] + k [N][Bc][2]; the
+// ABI-layout plan Xs [N+1][4][B] (copy_out's target) follows the records.
+struct RArgs {
+  int B, i0, Bc, H;
+  real success_r;
+  const real* x0;  // [3][B]
+  real* U;         // [N][2][B] warm start in, the last shifted plan out
+  real* Xs;        // [N+1][4][B] the plan in the ABI layout (scratch)
+  real* log;       // [H][6][B]
+  int* h_ran;
+  int* success_t;
+  int* collided;
+  int* status;
+  real* work;
+  unsigned wsz, oX, oU, oK, ok;
+};
+struct RK {
+  FP p;
+  FCost c;
+  FIlqr cf;
+  RArgs a;
+};
+__device__ __forceinline__ const RK* rkargs() {
+  __attribute__((address_space(4))) const RK* k =
+      (__attribute__((address_space(4))) const RK*)__builtin_amdgcn_kernarg_segment_ptr();
+  __asm__ volatile("" : "+s"(k));
+  return (const RK*)k;
+}
+
+// the true min_i h_i over the circles (run_nominal.py:388-397), rounded as h_circle_exact (no contraction)
+template <int M>
+__device__ __forceinline__ real h_true_min(const FP& p, real px, real py) {
+#pragma clang fp contract(off)
+  real m = 0.f;
+#pragma unroll
+  for (int i = 0; i < Obs<M>::n; ++i) {
+    const real dx = px - p.cx[i], dy = py - p.cy[i];
+    const real hi = dx * dx + dy * dy - p.r2[i];
+    m = i == 0 ? hi : m_min(m, hi);
+  }
+  return m;
+}
+
+template <int M, int GM>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
+receding_fast_kernel(RK kk) {
+  constexpr bool G0 = GM > 0, RG0 = GM > 1;
+  constexpr int MW = M | kWrap;
+  (void)kk;  // read through rkargs()
+  const RArgs& a = rkargs()->a;
+  const int B = a.B, Bc = a.Bc, i0 = a.i0;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = i0 + t;
+  if (t >= Bc) return;
+  const size_t nb = (size_t)B;
+  const unsigned lo = (unsigned)i * (4u * ES), bb = (unsigned)B * (4u * ES);
+  const Lane L{lo, lo + bb, lo + 2u * bb, lo + 3u * bb};
+  const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * (8u * ES), l16 = (unsigned)t * (16u * ES), l32 = (unsigned)t * (32u * ES);
+  const SlotMap sm{l16, cb * (16u * ES), l8, cb * (8u * ES)};
+  Solve<false, G0, RG0, 1> S;
+  S.r = __builtin_amdgcn_make_buffer_rsrc(a.work, 0, (int)a.wsz, 0x00020000);
+  S.XA = RA{a.oX, cb * (16u * ES), l16};
+  S.UA = RA{a.oU, cb * (8u * ES), l8};
+  S.XRA = S.XA;
+  S.URA = S.UA;
+  S.G.K = RA{a.oK, cb * (32u * ES), l32};
+  S.G.k = RA{a.ok, cb * (8u * ES), l8};
+  S.X = Soa<4>{(char*)a.Xs, 4u * bb, L};
+  S.U = Soa<2>{(char*)a.U, 2u * bb, L};
+  const FP p = pin_p<M>(rkargs()->p);
+  const FCost c = rkargs()->c;
+  const FIlqr cf = rkargs()->cf;
+  const int N = p.N, H = a.H;
+  real x[4] = {a.x0[i], a.x0[nb + i], a.x0[2 * nb + i], 0.f};
+  x[3] = barrier_at<M>(p, x[0], x[1]);  // dbas_init_b0 (run_nominal.py:279)
+  int st = 0, ran = H, sidx = -1, coll = 0;
+  for (int ts = 0; ts < H; ++ts) {
+    int it = 0;
+    Prof pf;
+    st |= ilqr<false, MW, 1, false>(p, c, cf, x, S, 0, sm, it, pf, DecRec{nullptr, nullptr, 0});
+    const f2 u = rld2(S.r, S.UA, 0, 0);  // the plan's first control (the records hold the solved plan)
+    real* lg = a.log + (size_t)ts * 6 * nb + i;
+    lg[0] = x[0];
+    lg[nb] = x[1];
+    lg[2 * nb] = x[2];
+    lg[3 * nb] = u.x;
+    lg[4 * nb] = u.y;
+    lg[5 * nb] = x[3];
+    if (st) {
+      ran = ts + 1;
+      break;
+    }
+    if (h_true_min<M>(p, x[0], x[1]) <= real(0)) {  // collision (run_nominal.py:388-397)
+      coll = 1;
+      ran = ts + 1;
+      break;
+    }
+    {
+      DTMPC_NOCONTRACT
+      const real ex = x[0] - c.tg.x, ey = x[1] - c.tg.y;
+      if (sqrt(ex * ex + ey * ey) <= a.success_r) {  // success (run_nominal.py:399-403)
+        sidx = ts;
+        ran = ts + 1;
+        break;
+      }
+    }
+    // x <- f_hat(x, u0) (run_nominal.py:377-378)
+    real Bc = barrier_at<M>(p, x[0], x[1]);
+    fhat<M, G0>(p, x[0], x[1], x[2], x[3], u.x, u.y, Bc);
+    // U <- [U[1:], U[-1]] (run_nominal.py:405-406) on the ABI warm start the next solve starts from
+    for (int k = 0; k + 1 < N; ++k) {
+      S.U.st(k, 0, S.U.ld(k + 1, 0));
+      S.U.st(k, 1, S.U.ld(k + 1, 1));
+    }
+  }
+  a.h_ran[i] = ran;
+  a.success_t[i] = sidx;
+  a.collided[i] = coll;
+  a.status[i] |= st;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2452,7 +2593,6 @@ template <int M, int P, int NCV>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 general_solve_fast_kernel(GSK kk) {
   (void)kk;  // read through gskargs()
-  __shared__ f4 lds[1];
   const GSArgs& a = gskargs()->a;
   const int B = a.B, Bc = a.Bc, i0 = a.i0;
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2467,8 +2607,6 @@ general_solve_fast_kernel(GSK kk) {
   const SlotMap sm{l16, cb * (16u * ES), l8, cb * (8u * ES)};
   const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * (16u * ES) : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * (8u * ES) : l8;
   Gains<P> G;
-  G.L = (lf4*)lds + (threadIdx.x / P);
-  G.w = h == 0;
   G.K = RA{a.oK, cb * (32u * ES), l32};
   G.k = RA{a.ok, cb * (8u * ES), l8};
   const Rsrc r = __builtin_amdgcn_make_buffer_rsrc(a.work, 0, (int)a.wsz, 0x00020000);
@@ -2821,6 +2959,79 @@ int FKN(launch_ilqr_fast)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmp
 #undef IL_LAUNCH
   }
   return check_launch("ilqr_fast_kernel");
+}
+
+// the receding-horizon driver on the same solver (dtmpc_nominal_receding): the fast configuration with the
+// nominal target cost, wrapped or not, one lane per trajectory
+bool FKN(receding_fast_eligible)(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf) {
+  const char* e = getenv("DTMPC_FAST");
+  if (e && e[0] == '0' && e[1] == 0) return false;
+  if (DTMPC_FAST_F64 && (e = getenv("DTMPC_FAST64")) && e[0] == '0' && e[1] == 0) return false;
+  if (dtype != kFastDtype || !fast_spec_ok(sp) || c->kind != DTMPC_COST_TARGET) return false;
+  return make_ilqr<real>(*cf).nc == FK_NS::NC;
+}
+static int64_t receding_fast_bytes_per_traj(int N) {  // records X, U, K, k + the ABI-layout plan
+  return (int64_t)(N + 1) * 16 * ES + (int64_t)N * 8 * ES + (int64_t)N * 40 * ES + (int64_t)(N + 1) * 16 * ES;
+}
+size_t FKN(receding_fast_workspace_bytes)(int N, int64_t B) { return (size_t)B * (size_t)receding_fast_bytes_per_traj(N); }
+
+int FKN(launch_receding_fast)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, int H,
+                              double success_r, const void* x0, void* U, void* log, int* h_ran, int* success_t,
+                              int* collided, int* status, void* work, hipStream_t st) {
+  const int N = sp->horizon;
+  FK_NS::RK kk;
+  std::memset(&kk, 0, sizeof(kk));
+  fast_p(sp, kk.p);
+  const DCost<real> c = make_cost<real>(*cp);
+  kk.c = FK_NS::FCost{c.Q0, c.Q1, c.Q2, c.R0, c.R1, c.Qf0, c.Qf1, c.Qf2, c.qb, FK_NS::f4{c.t0, c.t1, c.t2, 0.f}};
+  kk.cf = fast_ilqr(*cf);
+  FK_NS::RArgs& a = kk.a;
+  a.B = (int)B;
+  a.H = H;
+  a.success_r = real(success_r);
+  a.x0 = (const real*)x0;
+  a.U = (real*)U;
+  a.log = (real*)log;
+  a.h_ran = h_ran;
+  a.success_t = success_t;
+  a.collided = collided;
+  a.status = status;
+  // the ABI-layout plan after every chunk's records (the records of one chunk below 2^31 bytes)
+  const int64_t rec = receding_fast_bytes_per_traj(N) - (int64_t)(N + 1) * 16 * ES;
+  const int64_t chunk = ((int64_t)0x7fffffff / rec) / kBlock * kBlock;
+  a.Xs = (real*)((char*)work + (size_t)B * (size_t)rec);
+  a.work = (real*)work;
+  const int g0 = kk.p.gamma == 0.f ? 2 : 0;
+  for (int64_t c0 = 0; c0 < B; c0 += chunk) {
+    const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
+    a.i0 = (int)c0;
+    a.Bc = (int)Bc;
+    a.work = (real*)((char*)work + (size_t)c0 * (size_t)rec);
+    a.oX = 0;
+    a.oU = (unsigned)(Bc * (N + 1) * 16 * ES);
+    a.oK = a.oU + (unsigned)(Bc * N * 8 * ES);
+    a.ok = a.oK + (unsigned)(Bc * N * 32 * ES);
+    a.wsz = a.ok + (unsigned)(Bc * N * 8 * ES);
+    const int bs = tube_block(B, 1);
+    const dim3 grid = dim3((unsigned)((Bc + bs - 1) / bs));
+#define RC_LAUNCH(m, g) hipLaunchKernelGGL((FK_NS::receding_fast_kernel<m, g>), grid, dim3(bs), 0, st, kk)
+#define RC_CASE(m) \
+  case m:          \
+    if (g0 == 2) RC_LAUNCH(m, 2); else RC_LAUNCH(m, 0); break;
+    switch (sp->n_obstacles) {
+#if defined(DTMPC_FAST_M_ONLY)
+      RC_CASE(DTMPC_FAST_M_ONLY)
+#elif defined(DTMPC_FAST_ISA_ONLY)
+      RC_CASE(5)
+#else
+      RC_CASE(1) RC_CASE(2) RC_CASE(3) RC_CASE(4) RC_CASE(5) RC_CASE(6) RC_CASE(7) RC_CASE(8)
+#endif
+      default: return set_err(DTMPC_ERR_BAD_ARG, "fast receding: obstacle count not instantiated");
+    }
+#undef RC_CASE
+#undef RC_LAUNCH
+  }
+  return check_launch("receding_fast_kernel");
 }
 
 #else  // the general path's solves (csrc/dtmpc_fast_general.hip)

@@ -202,6 +202,17 @@ size_t ilqr_fast_workspace_bytes64(int N, int64_t B, int lanes);
 int launch_ilqr_fast64(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, const void* x0,
                        const void* Xref, const void* Uref, void* X, void* U, void* K, void* kff, int* iters, int* status,
                        signed char* choices, void* costs, int lanes, void* work, size_t work_bytes, hipStream_t st);
+// the receding-horizon driver on the same solver (dtmpc_nominal_receding), f32 and f64 (dtmpc_fast*_ilqr.hip)
+bool receding_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf);
+size_t receding_fast_workspace_bytes(int N, int64_t B);
+int launch_receding_fast(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, int H,
+                         double success_r, const void* x0, void* U, void* log, int* h_ran, int* success_t,
+                         int* collided, int* status, void* work, hipStream_t st);
+bool receding_fast_eligible64(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf);
+size_t receding_fast_workspace_bytes64(int N, int64_t B);
+int launch_receding_fast64(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, int H,
+                           double success_r, const void* x0, void* U, void* log, int* h_ran, int* success_t,
+                           int* collided, int* status, void* work, hipStream_t st);
 // the general path's two solves on the same solver (dtmpc_general_step); per-trajectory solve status to sst
 bool general_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_general_cfg* cf);
 int launch_general_solve_fast(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int64_t B,

@@ -136,8 +136,12 @@ using namespace dtmpc;
 extern "C" {
 
 size_t dtmpc_receding_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
+  if (horizon < 1 || B < 1) return 0;
   size_t el = dtype == DTMPC_F64 ? 8 : 4;
-  return el * ((size_t)(horizon + 1) * 4 + (size_t)horizon * 10) * (size_t)B;
+  const size_t generic = el * ((size_t)(horizon + 1) * 4 + (size_t)horizon * 10) * (size_t)B;
+  // the fused driver's records (csrc/dtmpc_fast.hip receding_fast_kernel) need more: the larger of the two
+  const size_t fused = dtype == DTMPC_F64 ? receding_fast_workspace_bytes64(horizon, B) : receding_fast_workspace_bytes(horizon, B);
+  return generic > fused ? generic : fused;
 }
 
 int dtmpc_nominal_receding(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, const dtmpc_ilqr_cfg* cfg,
@@ -153,6 +157,13 @@ int dtmpc_nominal_receding(int dtype, const dtmpc_spec* spec, const dtmpc_cost* 
   if (!x0 || !U || !log || !h_ran || !success_t || !collided || !status || !work)
     return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
   hipStream_t st = (hipStream_t)stream;
+  // the paper configuration on the fused solver (DTMPC_FAST=0 / DTMPC_FAST64=0: the generic one below)
+  if (receding_fast_eligible(dtype, spec, cost, cfg))
+    return launch_receding_fast(spec, cost, cfg, B, H, success_radius, x0, U, log, h_ran, success_t, collided, status,
+                                work, st);
+  if (receding_fast_eligible64(dtype, spec, cost, cfg))
+    return launch_receding_fast64(spec, cost, cfg, B, H, success_radius, x0, U, log, h_ran, success_t, collided,
+                                  status, work, st);
   if (dtype == DTMPC_F32)
     return launch_receding<float>(spec, cost, cfg, B, H, success_radius, x0, U, log, h_ran, success_t, collided, status,
                                   work, st);

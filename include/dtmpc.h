@@ -470,7 +470,10 @@ size_t dtmpc_receding_workspace_bytes(int dtype, int32_t horizon, int64_t B);
  * (:399-403).  x0 [3][B] (b0 = B(h(x0)) is derived, :279); U [N][2][B] warm start in (the reference
  * uses v = v_max, omega = 0, :368-369), last shifted plan out; log [H][6][B] out: x(3), u0(2), b of
  * every recorded step (rows past h_ran untouched); h_ran / success_t (-1: none) / collided [B] out;
- * status [B] OR-accumulated (a failed solve ends that trajectory's run, where the reference raises). */
+ * status [B] OR-accumulated (a failed solve ends that trajectory's run, where the reference raises).
+ * The paper configuration (smooth-min obstacles, relaxed inverse barrier, six non-zero alphas + 0) runs the
+ * tube step's fused solver with the wrapped cost compiled in (csrc/dtmpc_fast.hip receding_fast_kernel, f32
+ * and f64); anything else, and DTMPC_FAST=0 / DTMPC_FAST64=0, the generic receding_kernel. */
 int dtmpc_nominal_receding(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
                            const dtmpc_ilqr_cfg* cfg, int64_t B, int32_t H, double success_radius,
                            const void* x0, void* U, void* log, int32_t* h_ran, int32_t* success_t,

@@ -54,20 +54,25 @@ def kernel_stats(root, kern):
 def main():
     root, out = sys.argv[1], sys.argv[2]
     batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 65536
-    tube = {k: v for sub in ("fetch", "write", "sq1", "sq2", "tcc") for k, v in counters(root, TUBE_KERNELS, sub).items()}
+    # --kernel SUBSTR / --workload NAME: another kernel of the run, e.g. the f64 leg (fk64::tube_fast_kernel,
+    # workload tube_f64: bench.py's tube_f64 roofline reads it; its record loads are all 16 B per lane, the
+    # width the calibration launch's reads mostly have)
+    kern = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else TUBE_KERNELS
+    workload = sys.argv[sys.argv.index("--workload") + 1] if "--workload" in sys.argv else "tube"
+    tube = {k: v for sub in ("fetch", "write", "sq1", "sq2", "tcc") for k, v in counters(root, kern, sub).items()}
     cal_f = counters(root, "record_stream_kernel", "cal_fetch")
     cal_w = counters(root, "record_stream_kernel", "cal_write")
     N = 50
     Bc = 262144
     known_r = known_w = Bc * ((N + 1) * 16 + N * 8)
-    ks = kernel_stats(root, TUBE_KERNELS)
+    ks = kernel_stats(root, kern)
     import hashlib
 
     lib = os.environ.get("DTMPC_LIBRARY") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                           "differentiable-tube-mpc_amd", "diff_tube_mpc_strict_pt",
                                                           "libdtmpc.so")
     res = {"kernel": (ks or {}).get("name", "tube step") + " (7 alphas: 6 rolled out + alpha = 0 from the current tape)",
-           "workload": "tube", "batch": batch, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
+           "workload": workload, "batch": batch, "lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(),
            "counters_per_dispatch": tube, "kernel_trace": ks}
     if "FETCH_SIZE" in tube and "WRITE_SIZE" in tube:
         raw = 1024.0 * (tube["FETCH_SIZE"] + tube["WRITE_SIZE"])

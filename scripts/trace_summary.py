@@ -13,6 +13,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("trace")
 ap.add_argument("out")
 ap.add_argument("--warmup", type=int, required=True)
+ap.add_argument("--timed-last", type=int, default=0,
+                help="take the LAST K launches as the timed ones (bench.py warms up until the clock is stable, "
+                     "so the warm-up count varies; its timed steps are the last --steps launches)")
 ap.add_argument("--kernel", default="fk::tube_fast_kernel")  # f32 (fk64:: is the f64 leg)
 ap.add_argument("--batch", type=int, default=65536)
 ap.add_argument("--algo-bytes", type=float, default=274324.0 * 65536)
@@ -24,7 +27,9 @@ for f in glob.glob(os.path.join(a.trace, "**", "*kernel_trace.csv"), recursive=T
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:100]))
 rows.sort()
 d = [(e - s) * 1e-6 for s, e, _ in rows]  # ms
-timed = d[a.warmup:]
+timed = d[-a.timed_last:] if a.timed_last > 0 else d[a.warmup:]
+if a.timed_last > 0:
+    a.warmup = len(d) - len(timed)
 mean = sum(timed) / len(timed)
 res = {"kernel": rows[0][2] if rows else a.kernel, "launches": len(d), "warmup_excluded": a.warmup,
        "timed_launches": len(timed), "mean_ms": mean, "min_ms": min(timed), "max_ms": max(timed),
