@@ -126,20 +126,49 @@ def decision_agreement(dev_ch, oracle_chs, dev_U=None, oracle_Us=None, label: st
 
 # --------------------------------------------------------------------------------------------------------
 # f32 against f64 truth, and the tie-aware decision gate (VERDICT r03 "next" #1)
-def f64_truth(dev_out, build_outs, truth, k: float = 1.5, floor: float = 2e-5):
-    """Per trajectory: the device's f32 error against the f64 oracle (the truth: the reference's configured
-    precision, configs/dubins.yaml:8) must be no worse than k x the worst f32 oracle build's error against
-    the same truth (floor: below it every f32 evaluation is at rounding level -- a ratio of two rounding
-    noises says nothing).  Also the fraction within SURVEY.md §8c's 1e-3 for the device and every build.
-    Returns dict(frac_ok, e_dev, e_worst, within_1e3_dev, within_1e3_builds)."""
-    e_dev = rel_rows(dev_out, truth)
+def f64_truth(dev_out, build_outs, truth, floor: float = 2e-5, k_q=(2.0, 2.0, 5.0), slack: float = 0.03):
+    """f32 against f64 truth: is the device's f32 result as close to the f64 oracle (the
+    reference's configured precision, configs/dubins.yaml:8) as a valid f32 evaluation of the same algorithm?
+
+    Per trajectory, e = rel error against the f64 result, for the device and for each f32 oracle build.  The
+    question is distributional: the three builds -- three valid f32 roundings -- are themselves each other's
+    worst on a sizeable share of the chaotic trajectories (measured on the bench-mode tube step, B = 700:
+    one build's error exceeds 1.5 x the other two's on 3 % (x) to 11-31 % (plans, gradients) of them, with
+    ratios up to ~2000; scripts/calib_f32_truth.py), so a per-trajectory "within 1.5 x the worst build on
+    99 %" is not a property of f32 arithmetic.  The gate is therefore:
+      (a) worst-of-all share: the device's error exceeds every build's (and the floor) on no more trajectories
+          than the worst-of-three share of the builds among themselves (+ slack);
+      (b) quantiles: the device's median / p90 / p99 error is within k_q = 2 / 2 / 5 x the largest build's
+          (p99 of ~700 trajectories is their top 7: a few chaotic ones);
+      (c) SURVEY §8c's 1e-3: the device's share within 1e-3 of f64 is within `slack` of the lowest build's.
+    Returns a dict with each figure and frac_ok (1.0 when all three hold, else the failing share)."""
+    e_dev = np.maximum(rel_rows(dev_out, truth), 0.0)
     e_b = np.stack([rel_rows(o, truth) for o in build_outs])
-    worst = e_b.max(0)
-    ok = e_dev <= np.maximum(k * worst, floor)
-    return {"frac_ok": float(ok.mean()), "e_dev": e_dev, "e_worst": worst,
-            "within_1e3_dev": float((e_dev <= 1e-3).mean()),
-            "within_1e3_builds": [float((e <= 1e-3).mean()) for e in e_b],
-            "bad": np.nonzero(~ok)[0].tolist()}
+    worst_all = (e_dev > e_b.max(0)) & (e_dev > floor)
+    n = len(build_outs)
+    bw = [float(np.mean((e_b[i] > np.max(np.delete(e_b, i, 0), 0)) & (e_b[i] > floor))) for i in range(n)]
+    qs = (0.5, 0.9, 0.99)
+    qd = np.quantile(np.maximum(e_dev, floor), qs)
+    qb = np.max(np.quantile(np.maximum(e_b, floor), qs, axis=1), axis=1)
+    w_dev = float((e_dev <= 1e-3).mean())
+    w_b = [float((e <= 1e-3).mean()) for e in e_b]
+    ok_a = float(worst_all.mean()) <= max(bw) + slack
+    ok_b = bool(np.all(qd <= np.asarray(k_q) * qb))
+    ok_c = w_dev >= min(w_b) - slack
+    return {"frac_ok": 1.0 if (ok_a and ok_b and ok_c) else 0.0, "ok": (ok_a, ok_b, ok_c),
+            "dev_worst_of_all": float(worst_all.mean()), "builds_worst_of_rest": bw,
+            "quantiles_dev": qd.tolist(), "quantiles_builds_max": qb.tolist(),
+            "within_1e3_dev": w_dev, "within_1e3_builds": w_b, "e_dev": e_dev,
+            "bad": np.nonzero(worst_all)[0].tolist()}
+
+
+def f64_truth_line(res) -> str:
+    return (f"device worst of all {res['dev_worst_of_all']:.3f} (builds' worst-of-rest "
+            + " ".join(f"{v:.3f}" for v in res["builds_worst_of_rest"])
+            + f"); quantiles dev " + " ".join(f"{v:.2g}" for v in res["quantiles_dev"])
+            + " vs builds " + " ".join(f"{v:.2g}" for v in res["quantiles_builds_max"])
+            + f"; within 1e-3: device {res['within_1e3_dev']:.4f}, builds "
+            + " ".join(f"{v:.4f}" for v in res["within_1e3_builds"]) + f" -> {'ok' if res['frac_ok'] else 'FAIL'} {res['ok']}")
 
 
 def _ulp32(J):

@@ -13,8 +13,8 @@ import numpy as np
 import pytest
 import torch
 
-from _common import (CHAOTIC, agreement, decision_agreement, f64_truth, golden, ilqr_cfg, oracles, paper_setup, rel,
-                     tie_aware_decisions, tol_for)
+from _common import (CHAOTIC, agreement, decision_agreement, f64_truth, f64_truth_line, golden, ilqr_cfg, oracles,
+                     paper_setup, rel, tie_aware_decisions, tol_for)
 
 pytestmark = pytest.mark.gpu
 
@@ -238,11 +238,13 @@ def test_ilqr_batched_vs_oracle(dev, oracle_lib, tag, variant, monkeypatch):
     assert dec["on_determinate"] >= DECISION_GATE_TRACK[tag], dec
 
 
-# f32 against f64 truth: the device's f32 solution must be no further from the f64 oracle
-# (the reference's configured precision) than 1.5 x the worst of the three f32 oracle builds, per trajectory,
-# on >= 99 % (floor 2e-5: both at rounding level); and its line-search decisions must equal a build's or split
-# from it only at a near-tie (tests/_common.tie_aware_decisions), on >= 99 %.
-F32_TRUTH_GATE = 0.99
+# f32 against f64 truth: the device's f32 solution must be as close to the f64 oracle (the
+# reference's configured precision) as a valid f32 evaluation is -- no more often the worst than the builds are
+# among themselves, quantiles within 2 x the builds', the §8c 1e-3 share within 3 points of the lowest build's
+# (tests/_common.f64_truth; the per-trajectory "1.5 x the worst build on 99 %" fails for the builds themselves,
+# scripts/calib_f32_truth.py) -- and its line-search decisions must equal a build's or split from it only at a
+# near-tie (tests/_common.tie_aware_decisions), on >= 99 % (the builds among themselves: 0.996-0.999).
+F32_TRUTH_GATE = 1.0
 TIE_GATE = 0.99
 
 
@@ -250,10 +252,8 @@ def _f32_vs_truth(r, outs, truth, tol, fused, label):
     keep = (outs[0][5] == 0) & (r.status.cpu().numpy() == 0) & (truth[5] == 0)
     for name, dv, k in (("X", r.X, 0), ("U", r.V, 1)):
         res = f64_truth(dv.cpu().numpy()[keep], [o[k][keep] for o in outs], truth[k][keep])
-        print(f"[f32 vs f64 truth {label}] {name}: {res['frac_ok']:.4f} within 1.5 x the worst f32 build; "
-              f"within 1e-3 of f64: device {res['within_1e3_dev']:.4f}, builds "
-              + " ".join(f"{v:.4f}" for v in res["within_1e3_builds"]))
-        assert res["frac_ok"] >= F32_TRUTH_GATE, (label, name, res["frac_ok"], res["bad"][:8])
+        print(f"[f32 vs f64 truth {label}] {name}: " + f64_truth_line(res))
+        assert res["frac_ok"] >= F32_TRUTH_GATE, (label, name, f64_truth_line(res), res["bad"][:8])
     if fused:  # the candidate-cost record is written by the fused solver
         tie = tie_aware_decisions(r.choices.cpu().numpy()[keep], r.costs.cpu().numpy()[keep],
                                   [o[6][keep] for o in outs], [o[7][keep] for o in outs], tol=tol, label=label)
@@ -479,10 +479,8 @@ def test_tube_step_vs_oracle(dev, oracle_lib, tag, mode, lanes, monkeypatch):
                     f = lambda a: np.transpose(a, (2, 0, 1))  # noqa: E731
                     dv, bo, tr = f(getattr(mpc, k).cpu().numpy()), [f(o_[0][k]) for o_ in outs], f(tstate[k])
                 res = f64_truth(dv[kt], [b_[kt] for b_ in bo], tr[kt])
-                print(f"[f32 vs f64 truth {lab}] {k}: {res['frac_ok']:.4f} within 1.5 x the worst f32 build; "
-                      f"within 1e-3 of f64: device {res['within_1e3_dev']:.4f}, builds "
-                      + " ".join(f"{v:.4f}" for v in res["within_1e3_builds"]))
-                assert res["frac_ok"] >= F32_TRUTH_GATE, (lab, k, res["frac_ok"], res["bad"][:8])
+                print(f"[f32 vs f64 truth {lab}] {k}: " + f64_truth_line(res))
+                assert res["frac_ok"] >= F32_TRUTH_GATE, (lab, k, f64_truth_line(res), res["bad"][:8])
             tie = tie_aware_decisions(mpc.choices.cpu().numpy().T[keep],
                                       np.transpose(mpc.costs.cpu().numpy(), (2, 0, 1))[keep],
                                       [o_[4].T[keep] for o_ in outs], [o_[5][keep] for o_ in outs],
