@@ -20,6 +20,7 @@ arguments.  There is no CPU fallback: tensors must live on a HIP device.
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 from dataclasses import dataclass
 from typing import Optional
 
@@ -118,8 +119,20 @@ def _prep_x0(x0: Tensor) -> Tensor:
     return x0.t().contiguous()
 
 
-def rollout(problem: DubinsDBaSProblem, x0: Tensor, V: Tensor) -> Tensor:
-    """X[k+1] = f_hat(X[k], V[k]) for every trajectory (core/ddp.py:89-99, f = DBaS step)."""
+def rollout(problem, x0: Tensor, V: Optional[Tensor] = None, *, f=None) -> Tensor:
+    """X[k+1] = f_hat(X[k], V[k]) for every trajectory (core/ddp.py:89-99, f = DBaS step).
+
+    Typed form rollout(problem, x0 [B, 4], V [B, N, 2]); the reference's form rollout(x0, V, *, f) with f a
+    core.closures.DBaSDynamics (x0 [4] / V [N, 2], or batched)."""
+    if f is not None:
+        from .closures import DBaSDynamics, _owner
+
+        dyn = _owner(f, DBaSDynamics, "f")
+        x0_, V_ = problem, x0
+        single = x0_.ndim == 1
+        xb, Vb = (x0_[None], V_[None]) if single else (x0_, V_)
+        out = rollout(dataclasses.replace(dyn.problem, horizon=Vb.shape[1]), xb, Vb)
+        return out[0] if single else out
     _require_device(x0, V)
     B, N = x0.shape[0], problem.horizon
     if V.shape != (B, N, 2):
@@ -168,11 +181,17 @@ def linearize(problem: DubinsDBaSProblem, cost: QuadraticCost, X: Tensor, V: Ten
     return (from_soa(A).view(Bsz, N, 4, 4), from_soa(Bm).view(Bsz, N, 4, 2), from_soa(lx), from_soa(lu))
 
 
-def ilqr_solve(*, problem: DubinsDBaSProblem, cost: QuadraticCost, cfg: ILQRConfig, x0: Tensor,
-               V_init: Tensor, X_ref: Optional[Tensor] = None, U_ref: Optional[Tensor] = None,
-               check: bool = True, debug_name: str = "ilqr", record_choices: bool = False,
-               lanes: int = 0, record_costs: bool = False) -> ILQRResult:
+def ilqr_solve(*, problem: Optional[DubinsDBaSProblem] = None, cost: Optional[QuadraticCost] = None,
+               cfg: ILQRConfig, x0: Tensor, V_init: Tensor, X_ref: Optional[Tensor] = None,
+               U_ref: Optional[Tensor] = None, check: bool = True, debug_name: str = "ilqr",
+               record_choices: bool = False, lanes: int = 0, record_costs: bool = False,
+               f=None, f_jac=None, ctrl=None, stage_cost=None, terminal_cost=None, stage_derivs=None,
+               terminal_derivs=None, feasible_fn=None, debug: bool = False):
     """Batched box-clamped iLQR (core/ddp.py:102-307).
+
+    The reference's keyword form -- ilqr_solve(x0=, V_init=, cfg=, f=, f_jac=, ctrl=, stage_cost=,
+    terminal_cost=, stage_derivs=, terminal_derivs=) with closures from core.closures -- is resolved to this
+    typed call and returns the reference's (X*, V*) pair (unbatched for x0 [4], V_init [N, 2]).
 
     x0 [B, 4], V_init [B, N, 2] (not mutated), X_ref [B, N+1, >=3] / U_ref [B, N, 2] for the tracking
     cost.  Returns X* [B, N+1, 4], V* [B, N, 2] and diagnostics; record_choices adds the decision
@@ -183,6 +202,23 @@ def ilqr_solve(*, problem: DubinsDBaSProblem, cost: QuadraticCost, cfg: ILQRConf
     csrc/dtmpc_fast_ilqr.hip / dtmpc_fast64_ilqr.hip; DTMPC_FAST=0 / DTMPC_FAST64=0 switch it off) with
     ``lanes`` lanes per trajectory (0: dtmpc_tube_lanes(B); 1, 2 or 4), else the generic kernel
     (dtmpc_ilqr_fused_eligible says which)."""
+    if f is not None:
+        if problem is not None or cost is not None:
+            raise TypeError("pass either problem / cost (typed form) or the closures (keyword form), not both")
+        from .closures import resolve_ilqr
+
+        r = resolve_ilqr(cfg=cfg, f=f, f_jac=f_jac, ctrl=ctrl, stage_cost=stage_cost, terminal_cost=terminal_cost,
+                         stage_derivs=stage_derivs, terminal_derivs=terminal_derivs, feasible_fn=feasible_fn)
+        single = x0.ndim == 1
+        xb, Vb = (x0[None], V_init[None]) if single else (x0, V_init)
+        Xr, Ur = r.X_ref, r.U_ref
+        if Xr is not None and Xr.ndim == 2:
+            Xr, Ur = Xr[None].expand(xb.shape[0], *Xr.shape), Ur[None].expand(xb.shape[0], *Ur.shape)
+        res = ilqr_solve(problem=r.problem, cost=r.cost, cfg=cfg, x0=xb, V_init=Vb, X_ref=Xr, U_ref=Ur,
+                         check=True, debug_name=debug_name, lanes=lanes)
+        return (res.X[0], res.V[0]) if single else (res.X, res.V)
+    if problem is None or cost is None:
+        raise TypeError("ilqr_solve needs problem and cost (typed form) or f and the cost closures (keyword form)")
     _require_device(x0, V_init, X_ref, U_ref)
     B, N = x0.shape[0], problem.horizon
     if cfg.horizon != N:
@@ -223,16 +259,44 @@ def ilqr_solve(*, problem: DubinsDBaSProblem, cost: QuadraticCost, cfg: ILQRConf
                       costs=cr[:cfg.max_iter].permute(2, 0, 1).contiguous() if cr is not None else None)
 
 
-def ddp_sensitivity(*, problem: DubinsDBaSProblem, cost: QuadraticCost, X: Tensor, V: Tensor,
-                    X_ref: Optional[Tensor] = None, U_ref: Optional[Tensor] = None, X_bar: Optional[Tensor] = None,
-                    upper_grad_x: Optional[Tensor] = None, upper_grad_u: Optional[Tensor] = None,
-                    want_lambda: bool = True, check: bool = True) -> SensitivityResult:
+def ddp_sensitivity(*, problem: Optional[DubinsDBaSProblem] = None, cost: Optional[QuadraticCost] = None,
+                    X: Tensor, V: Tensor, X_ref: Optional[Tensor] = None, U_ref: Optional[Tensor] = None,
+                    X_bar: Optional[Tensor] = None, upper_grad_x=None, upper_grad_u=None,
+                    want_lambda: bool = True, check: bool = True, f=None, f_jac=None, ctrl=None,
+                    stage_hess=None, terminal_hess=None, upper_grad_xN=None) -> SensitivityResult:
     """DDP-structured KKT sensitivity with active set (core/ddp.py:317-427).
+
+    The reference's keyword form -- ddp_sensitivity(X=, V=, f=, f_jac=, ctrl=, stage_hess=, terminal_hess=,
+    upper_grad_x=, upper_grad_u=, upper_grad_xN=) with f / the Hessians from core.closures and the upper-level
+    gradients as callables (x, k) / (u, k) / (x_N), evaluated along the tape -- is resolved to the array
+    form below (unbatched result for X [N+1, 4]).
 
     Upper-level gradients either as arrays -- upper_grad_x [B, N+1, 4] (row N = upper_grad_xN) and
     upper_grad_u [B, N, 2], the reference's closures evaluated along the tape -- or, with X_bar, the
     paper upper loss L = sum ||x_k - xbar_k||^2 + b_k^2 (core/tube_mpc.py:915-957):
     g_x = [2(x - xbar), 2 b], g_u = 0."""
+    if f is not None:
+        if problem is not None or cost is not None:
+            raise TypeError("pass either problem / cost (typed form) or the closures (keyword form), not both")
+        from .closures import resolve_sensitivity
+
+        if not (callable(upper_grad_x) and callable(upper_grad_u) and callable(upper_grad_xN)):
+            raise TypeError("the keyword form takes upper_grad_x(x, k), upper_grad_u(u, k), upper_grad_xN(x_N)")
+        single = X.ndim == 2
+        Xb, Vb = (X[None], V[None]) if single else (X, V)
+        N = Vb.shape[1]
+        r = resolve_sensitivity(f=f, f_jac=f_jac, ctrl=ctrl, stage_hess=stage_hess, terminal_hess=terminal_hess,
+                                horizon=N)
+        gX = torch.stack([upper_grad_x(Xb[:, k], k) for k in range(N)] + [upper_grad_xN(Xb[:, N])], 1)
+        gU = torch.stack([upper_grad_u(Vb[:, k], k) for k in range(N)], 1)
+        res = _ddp_sensitivity_upper(r.problem, r.cost, Xb, Vb, gX.to(Xb).expand(Xb.shape[0], N + 1, 4),
+                                     gU.to(Xb).expand(Xb.shape[0], N, 2), want_lambda, check)
+        if not single:
+            return res
+        return SensitivityResult(delta_X=res.delta_X[0], delta_V=res.delta_V[0],
+                                 delta_lambda=res.delta_lambda[0] if res.delta_lambda is not None else None)
+    if problem is None or cost is None:
+        raise TypeError("ddp_sensitivity needs problem and cost (typed form) or f and the Hessian closures")
     if upper_grad_x is not None or upper_grad_u is not None:
         return _ddp_sensitivity_upper(problem, cost, X, V, upper_grad_x, upper_grad_u, want_lambda, check)
     if X_bar is None:

@@ -19,7 +19,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 LIB_PATHS = {"plain": LIB_PATH, "fma": os.path.join(HERE, "liboracle_fma.so"),
-             "ulp": os.path.join(HERE, "liboracle_ulp.so")}
+             "ulp": os.path.join(HERE, "liboracle_ulp.so"), "sym": os.path.join(HERE, "liboracle_sym.so")}
 _REPO = os.path.dirname(HERE)
 _PKG_ROOT = os.path.join(_REPO, "differentiable-tube-mpc_amd")
 if _PKG_ROOT not in sys.path:

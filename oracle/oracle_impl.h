@@ -437,6 +437,13 @@ static int FN(riccati_step)(const REAL* A, const REAL* Bm, const REAL* lx, const
       Vxx[i * 4 + j] = Qxx[i * 4 + j] + m1 + m2 + m3;
       ok &= FN(isfin)(Vxx[i * 4 + j]);
     }
+#ifdef ORACLE_SYM_VXX
+  /* test variant (liboracle_sym.so): V_xx mirrored from its upper triangle, the symmetric form the fused
+   * solver keeps (csrc/dtmpc_fast.hip riccati_pk); the reference's full recursion (core/ddp.py:252) lets the
+   * antisymmetric round-off grow by |A|^2 per step where the relaxed barrier's slope puts ~1e12 into A */
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < i; ++j) Vxx[i * 4 + j] = Vxx[j * 4 + i];
+#endif
   return ok ? 0 : 1;
 }
 

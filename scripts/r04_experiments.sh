@@ -4,7 +4,7 @@
 #  1. root cause, LDS general records: diag_g0 (B = 700 f32, 2 closed-loop steps) on lds0 / lds1 / lds0c / lds1c
 #  2. root cause, f64 inline far sincos: diag_g0 DT=f64 on far1 / far0 / far1c / far0c and the generic f64
 #     kernel, + test_tube_step_fast64_vs_generic[1] on far0 / far0c
-#  3. small batches: B = 4,096 four-lane tube step, prefetch lead 2 (lds0) / 3 / 4
+#  3. small batches: B = 4,096 four-lane tube step, prefetch lead 2 (the product library) / 3 / 4
 #  4. PMC at B = 4,096 (SQ issue / wait split)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -46,9 +46,13 @@ for v in far0 far0c; do
 done
 ;;
 lead)
-for v in lds0 lead3 lead4; do
+run b4096_lead2 300 env DTMPC_TUBE_LANES=4 python bench.py --batch 4096 --steps 20 --warmup 5 --no-cpu --no-steady --no-extra
+for v in lead3 lead4; do
   run b4096_$v 300 env DTMPC_LIBRARY=$PWD/$L/libdtmpc_$v.so DTMPC_TUBE_LANES=4 python bench.py --batch 4096 --steps 20 --warmup 5 --no-cpu --no-steady --no-extra
 done
+;;
+recdiag)
+run diag_receding 300 python scripts/diag_receding.py 1024
 ;;
 pmc)
 run pmc4096 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d "$OUT/pmc4096" -o run --output-format csv -- python3 bench.py --batch 4096 --steps 3 --warmup 1 --no-cpu --no-steady --no-extra

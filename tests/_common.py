@@ -247,6 +247,21 @@ def tie_aware_decisions(dev_ch, dev_costs, chs, costs, tol: float = -1.0, ulps: 
                 out = (score, kind, m, d, t)
         return out[1], out[2], out[3], out[4]
 
+    def rate_of(cA, JA, refs):  # the same rule for evaluation A against the evaluations refs
+        n_ok = 0
+        for i in range(B):
+            best = None
+            for cB, JB in refs:
+                t = _first_split(cA[i], cB[i])
+                if t < 0:
+                    best = 0.0
+                    break
+                kind, m, d = _split_margin(cA[i], JA[i], cB[i], JB[i], t, tol, t0_of(t))
+                sc = m / max(ulps, k_drift * d)
+                best = sc if best is None else min(best, sc)
+            n_ok += best is not None and best <= 1.0
+        return n_ok / B
+
     for i in range(B):
         kind, m, d, t = best_split(dev_ch, dev_costs, i)
         if kind == "exact":
@@ -259,6 +274,9 @@ def tie_aware_decisions(dev_ch, dev_costs, chs, costs, tol: float = -1.0, ulps: 
         else:
             res["fail"].append((i, kind, t, m, d))
     res["frac_ok"] = (res["exact"] + res["tie"]) / B
+    # the builds held to the same rule against the other builds: what valid roundings achieve on this batch
+    ev = list(zip(chs, costs))
+    res["builds_rate"] = [rate_of(cB, JB, [e for j, e in enumerate(ev) if j != b]) for b, (cB, JB) in enumerate(ev)]
     # calibration: build 1 and 2 against build 0 (the same measurement between valid roundings)
     cal = []
     for cB, JB in zip(chs[1:], costs[1:]):
@@ -274,7 +292,8 @@ def tie_aware_decisions(dev_ch, dev_costs, chs, costs, tol: float = -1.0, ulps: 
     print(f"[tie-aware decisions{(' ' + label) if label else ''}] B={B}: exact {res['exact']}, near-tie splits "
           f"{res['tie']}, failing {len(res['fail'])} -> {res['frac_ok']:.4f}; split margins (ulp of J) median "
           f"{res['margin_ulps_median']:.3g} p90 {res['margin_ulps_p90']:.3g}; builds among themselves median "
-          f"{res['builds_margin_ulps_median']:.3g} p90 {res['builds_margin_ulps_p90']:.3g}")
+          f"{res['builds_margin_ulps_median']:.3g} p90 {res['builds_margin_ulps_p90']:.3g}, builds' own pass rate "
+          + " ".join(f"{v:.4f}" for v in res["builds_rate"]))
     for f in res["fail"][:show]:
         print(f"    traj {f[0]}: {f[1]} split at iteration {f[2]}, margin {f[3]:.3g} ulp, drift {f[4]:.3g} ulp")
     return res

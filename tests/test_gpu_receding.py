@@ -116,96 +116,183 @@ def test_run_nominal_once(dev, tmp_path):
     assert res["summary"]["mode"] == "nominal_only"
 
 
-def test_receding_f32_failure_set_vs_oracle(dev, oracle_lib):
-    """The f32 receding driver's failure SET at scale: B = 4,096 runs of the benchmark's
-    start distribution (x0 ~ U[0,1]^2 x U[0, pi/2], paper configuration, H = 20), where about 10 % of the
-    runs end non-finite in f32 (a line-search candidate pushed deep into an obstacle overflows the relaxed
-    barrier's b^2, where the reference's f32 path raises FloatingPointError).
+def test_receding_f32_failure_set_vs_oracle(dev, oracle_lib, monkeypatch):
+    """The f32 receding driver's failure SET at scale: B = 4,096 runs of the
+    benchmark's start distribution (x0 ~ U[0,1]^2 x U[0, pi/2], paper configuration, H = 20).
 
-    Whether a run fails is a threshold event (a candidate's cost crossing 3.4e38), so the three oracle
-    builds -- the same algorithm in three valid roundings -- agree with EACH OTHER on only ~85 % of the runs
-    (measured: 0.851-0.856), and a 99 % device-vs-oracle agreement is not a property of the algorithm.  The
-    test pins what is: the device agrees with every build at least as well as the builds agree with each
-    other (minus 2 points), its failure count is within 15 % of theirs, and in f64 (no overflow) the failure
-    sets are identical (empty).  Round 3 (generic kernel): device-vs-build 0.832-0.843; failures 463 vs 416-425,
-    of them late in the horizon (h > 10) 100 vs ~51; the h > 10 split is asserted too since round 4 (the
-    driver on the fused solver)."""
+    Root cause of the reference's f32 failures (scripts/diag_receding.py): the warm start
+    (v = 10, w = 0) drives most of these runs straight into an obstacle, deep in the relaxed barrier's quadratic
+    branch, where A's barrier row carries dB/dh * dh/dx ~ 1e12.  The reference's V_xx recursion
+    (core/ddp.py:252, Q_xx + K^T Q_uu K + K^T Q_ux + Q_xu K, never symmetrised) rounds its (i, j) and (j, i)
+    entries in different orders; the antisymmetric part that leaves is not removed by the Schur complement
+    and is multiplied by ~|A|^2 per step, so two steps inside the obstacle overflow f32 (Q_uu = [[2, 1.9e34],
+    [-1.9e34, 3e25]] one step before the first non-finite gain).  The fused solver keeps V_xx symmetric
+    (upper triangle; csrc/dtmpc_fast.hip riccati_pk), so that mode does not exist there.  The oracle's
+    liboracle_sym.so (V_xx mirrored after every step, otherwise the plain build) separates the two: the
+    reference-form builds fail on ~10 % of the runs, the symmetric build on ~0.5 %.
+
+    Asserted: the reference-form builds' failure rate (the regime) and the symmetric build's; the device's
+    fused driver against the symmetric build (total and h > 10 counts within 15 % or 8 runs, the set agreeing
+    at least as well as the reference-form builds agree with each other); the generic kernel (DTMPC_FAST=0,
+    the reference's unsymmetrised form) against the reference-form builds (total within 15 %); f64: every
+    failure set identical (empty)."""
     import math
 
     from diff_tube_mpc_strict_pt.core import nominal_receding
     from diff_tube_mpc_strict_pt.core.receding import receding_setup_from_config
     from _common import config
+    from oracle.oracle import Oracle
 
     problem, cost, icfg = receding_setup_from_config(json.loads(json.dumps(config())))
     B, H, N = 4096, 20, problem.horizon
     g = torch.Generator().manual_seed(0)
     u = torch.rand(B, 3, generator=g, dtype=torch.float64)
     x0 = torch.stack([u[:, 0], u[:, 1], u[:, 2] * (math.pi / 2)], 1)
-    fails = {}
+    fails, hs = {}, {}
     for tag, tdt, npdt in (("f32", torch.float32, np.float32), ("f64", torch.float64, np.float64)):
-        r = nominal_receding(problem=problem, cost=cost, cfg=icfg, x0=x0.to(tdt).to(dev), H=H, check=False)
-        torch.cuda.synchronize()
+        devs = []
+        for fast in ("1", "0"):
+            monkeypatch.setenv("DTMPC_FAST", fast)
+            r = nominal_receding(problem=problem, cost=cost, cfg=icfg, x0=x0.to(tdt).to(dev), H=H, check=False)
+            torch.cuda.synchronize()
+            devs.append((r.status.cpu().numpy() != 0, r.h_ran.cpu().numpy()))
+        monkeypatch.delenv("DTMPC_FAST")
         U = np.zeros((B, N, 2), npdt)
         U[:, :, 0] = problem.u_max[0]
+        builds = oracles(npdt) + [Oracle(npdt, nthreads=8, variant="sym")]
         outs = [o.nominal_receding(problem.to_c(), cost.to_c(), icfg.to_c(), x0.numpy().astype(npdt), H, 0.25, U.copy())
-                for o in oracles(npdt)]
-        fails[tag] = [r.status.cpu().numpy() != 0] + [o[4] != 0 for o in outs]
-        if tag == "f32":
-            hs = [r.h_ran.cpu().numpy()] + [o[1] for o in outs]
-    f = fails["f32"]
-    inter = min(float((f[i] == f[j]).mean()) for i in range(1, 4) for j in range(i + 1, 4))
-    dev_vs = [float((f[0] == f[k]).mean()) for k in range(1, 4)]
+                for o in builds]
+        # [fused, generic, plain, fma, ulp, sym]
+        fails[tag] = [d[0] for d in devs] + [o[4] != 0 for o in outs]
+        hs[tag] = [d[1] for d in devs] + [o[1] for o in outs]
+    f, h = fails["f32"], hs["f32"]
     counts = [int(x.sum()) for x in f]
-    # where in the horizon the runs fail (VERDICT r03 #6: the h > 10 split): h_ran is the step of the failure
-    late = [int((fk & (hk > 10)).sum()) for fk, hk in zip(f, hs)]
-    print(f"[receding f32 B={B} H={H}] failures device / oracle builds {counts}, of them at h > 10 {late}; builds "
-          f"agree with each other >= {inter:.4f}; device agrees with each build {[round(v, 4) for v in dev_vs]}")
-    assert 0.02 <= f[0].mean() <= 0.3, f[0].mean()  # the regime the benchmark reports (~11 %)
-    assert min(dev_vs) >= inter - 0.02, (dev_vs, inter)
-    mean_or = np.mean(counts[1:])
-    assert abs(counts[0] - mean_or) <= 0.15 * mean_or, counts
-    mean_late = np.mean(late[1:])
-    assert abs(late[0] - mean_late) <= max(0.15 * mean_late, 8), late  # the late-horizon split too
-    assert all((x == fails["f64"][0]).all() for x in fails["f64"][1:])  # f64: the same (empty) set
+    late = [int((fk & (hk > 10)).sum()) for fk, hk in zip(f, h)]  # h_ran is the step of the failure
+    inter = min(float((f[i] == f[j]).mean()) for i in range(2, 5) for j in range(i + 1, 5))
+    print(f"[receding f32 B={B} H={H}] failures fused / generic / plain, fma, ulp builds / symmetric-V_xx build "
+          f"{counts}, of them at h > 10 {late}; reference-form builds agree with each other >= {inter:.4f}; "
+          f"fused vs symmetric build {float((f[0] == f[5]).mean()):.4f}")
+    assert all(0.02 <= x.mean() <= 0.3 for x in f[2:5]), counts  # the regime (the reference form, ~10 %)
+    assert f[5].mean() <= 0.015, counts  # ... of which the unsymmetrised V_xx accounts for ~95 %
+    assert abs(counts[0] - counts[5]) <= max(0.15 * counts[5], 8), counts
+    assert abs(late[0] - late[5]) <= max(0.15 * late[5], 8), late
+    assert float((f[0] == f[5]).mean()) >= inter - 0.02
+    mean_ref = np.mean(counts[2:5])
+    assert abs(counts[1] - mean_ref) <= 0.15 * mean_ref, counts  # the generic kernel keeps the reference form
+    assert all(not x.any() for x in fails["f64"]), [int(x.sum()) for x in fails["f64"]]  # f64: empty sets
 
 
 @pytest.mark.parametrize("tag", ["f64", "f32"])
-def test_receding_fused_vs_generic(dev, tag, monkeypatch):
+def test_receding_fused_vs_generic(dev, oracle_lib, tag, monkeypatch):
     """The receding driver on the tube step's fused solver (csrc/dtmpc_fast.hip receding_fast_kernel, the
-    wrapped target cost compiled in) against the generic receding_kernel (DTMPC_FAST=0) from the same starts:
-    the same algorithm in two roundings (the fused solver's FMA-contracted forward passes and its own sin /
-    cos), so exits are identical and the recorded runs agree to 1e-8 (f64) / 1e-4 (f32) relative on the
-    runs where no knife-edge exit intervenes (>= 97 % f64, >= 90 % f32)."""
+    wrapped target cost compiled in) against the generic receding_kernel (DTMPC_FAST=0) from the same starts
+    (x0 ~ U[0,3]^2 x U[0, pi/2], paper configuration, H = 20).
+
+    This workload is chaotic: many starts see an obstacle within the horizon and the closed loop passes close
+    to others, so the oracle's own builds (plain / fma / ulp: the same algorithm in three valid roundings)
+    agree on the exits of only ~80 % of the runs (f64) and on the whole recorded run at 1e-8 on only ~16 %
+    (measured 0.798-0.811 / 0.162-0.164).  The two device kernels are two more roundings: their agreement is
+    held to the builds' own (runs where nothing fails; minus 3 points for exits, 5 for the row fraction).
+    Row-level parity is pinned on the well-conditioned workloads above (the reference runs at 1e-9,
+    test_nominal_receding_batched_vs_oracle)."""
     import math
 
     from diff_tube_mpc_strict_pt.core import nominal_receding
     from diff_tube_mpc_strict_pt.core.receding import receding_setup_from_config
     from _common import config
 
-    tdt = torch.float64 if tag == "f64" else torch.float32
+    tdt, npdt = (torch.float64, np.float64) if tag == "f64" else (torch.float32, np.float32)
     problem, cost, icfg = receding_setup_from_config(json.loads(json.dumps(config())))
-    B, H = 1024, 20
+    B, H, N = 1024, 20, problem.horizon
     g = torch.Generator().manual_seed(5)
     u = torch.rand(B, 3, generator=g, dtype=torch.float64)
-    x0 = torch.stack([u[:, 0] * 3, u[:, 1] * 3, u[:, 2] * (math.pi / 2)], 1).to(tdt).to(dev)
+    x0 = torch.stack([u[:, 0] * 3, u[:, 1] * 3, u[:, 2] * (math.pi / 2)], 1)
     runs = []
     for fast in ("1", "0"):
         monkeypatch.setenv("DTMPC_FAST", fast)
-        r = nominal_receding(problem=problem, cost=cost, cfg=icfg, x0=x0, H=H, check=False)
+        r = nominal_receding(problem=problem, cost=cost, cfg=icfg, x0=x0.to(tdt).to(dev), H=H, check=False)
         torch.cuda.synchronize()
-        runs.append(r)
-    a, b = runs
-    ex = [np.stack([r.h_ran.cpu().numpy(), r.success_t.cpu().numpy(), r.collided.cpu().numpy()], 1) for r in runs]
-    same = (ex[0] == ex[1]).all(1) & (a.status.cpu().numpy() == 0) & (b.status.cpu().numpy() == 0)
-    la = torch.cat([a.x, a.u, a.b[..., None]], -1).cpu().numpy()
-    lb = torch.cat([b.x, b.u, b.b[..., None]], -1).cpu().numpy()
-    mask = np.arange(H)[None, :] < a.h_ran.cpu().numpy()[:, None]
-    d = np.where(mask[..., None], np.abs(la - lb), 0).reshape(B, -1).max(1)
-    sc = np.where(mask[..., None], np.abs(lb), 0).reshape(B, -1).max(1) + 1.0
+        runs.append((torch.cat([r.x, r.u, r.b[..., None]], -1).cpu().numpy(), r.h_ran.cpu().numpy(),
+                     r.success_t.cpu().numpy(), r.collided.cpu().numpy().astype(np.int32), r.status.cpu().numpy()))
+    monkeypatch.delenv("DTMPC_FAST")
+    U = np.zeros((B, N, 2), npdt)
+    U[:, :, 0] = problem.u_max[0]
+    for o in oracles(npdt):
+        runs.append(o.nominal_receding(problem.to_c(), cost.to_c(), icfg.to_c(), x0.numpy().astype(npdt), H, 0.25,
+                                       U.copy())[:5])
+    ok = np.all([r[4] == 0 for r in runs], axis=0)  # runs where nothing fails (f32: see the test above)
     tol = 1e-8 if tag == "f64" else 1e-4
-    frac_ex = float((ex[0] == ex[1]).all(1).mean())
-    frac = float((d[same] / sc[same] <= tol).mean())
-    print(f"[receding fused vs generic {tag}] exits equal {frac_ex:.4f}; runs within {tol:g} {frac:.4f} "
-          f"(of {int(same.sum())})")
-    need = 0.97 if tag == "f64" else 0.90
-    assert frac_ex >= need and frac >= need, (frac_ex, frac)
+
+    def pair(a, b):
+        ex = (a[1] == b[1]) & (a[2] == b[2]) & (a[3] == b[3])
+        same = ex & ok
+        mask = np.arange(H)[None, :] < a[1][:, None]
+        d = np.where(mask[..., None], np.abs(np.nan_to_num(a[0]) - np.nan_to_num(b[0])), 0).reshape(B, -1).max(1)
+        sc = np.where(mask[..., None], np.abs(np.nan_to_num(b[0])), 0).reshape(B, -1).max(1) + 1.0
+        return float(ex[ok].mean()), float((d[same] / sc[same] <= tol).mean())
+
+    dv = pair(runs[0], runs[1])
+    bl = [pair(runs[i], runs[j]) for i in range(2, 5) for j in range(i + 1, 5)]
+    print(f"[receding fused vs generic {tag}] on {int(ok.sum())} runs: exits equal {dv[0]:.4f}, runs within {tol:g} "
+          f"{dv[1]:.4f}; oracle builds pairwise {[(round(a, 4), round(b, 4)) for a, b in bl]}")
+    assert ok.mean() >= (1.0 if tag == "f64" else 0.8), ok.mean()
+    assert dv[0] >= min(b[0] for b in bl) - 0.03, (dv, bl)
+    assert dv[1] >= min(b[1] for b in bl) - 0.05, (dv, bl)
+
+
+def test_reference_call_pattern(dev):
+    """run_nominal.py:344-410 with its solver call (:353-364) in the reference's keyword form -- closures
+    from core.closures.nominal_closures, the f_jac lambda, single-trajectory tensors -- on the device in f64,
+    against the reference's own run (tests/golden/nominal_receding.npz, H = 2) at 1e-9."""
+    import math
+
+    from diff_tube_mpc_strict_pt.core import ilqr_solve
+    from diff_tube_mpc_strict_pt.core.closures import nominal_closures
+    from diff_tube_mpc_strict_pt.core.ddp import dbas_init
+    from _common import config
+
+    cfg = json.loads(json.dumps(config()))
+    cfg["system"]["task_horizon_H"] = 2
+    cl = nominal_closures(cfg)
+    f_hat, ctrl, ilqr_cfg, jac = cl["f_hat"], cl["ctrl"], cl["ilqr_cfg"], cl["f_jac"]
+    stage_cost, terminal_cost, stage_derivs, term_derivs = (cl["stage_cost"], cl["terminal_cost"],
+                                                            cl["stage_derivs"], cl["term_derivs"])
+    kw = dict(dtype=torch.float64, device=dev)
+    N, H = ilqr_cfg.horizon, 2
+    x = torch.tensor([0.0, 0.0, math.pi / 4], **kw)
+    b = dbas_init(f_hat.problem, x[None])[0]
+    U_ws = torch.zeros(N, 2, **kw)
+    U_ws[:, 0] = float(ctrl.u_max[0])
+    xs, us, bs = [], [], []
+    for t in range(H):
+        x_hat0 = torch.cat([x, b.view(1)], dim=0)
+        X_hat, U = ilqr_solve(
+            x0=x_hat0,
+            V_init=U_ws,
+            cfg=ilqr_cfg,
+            f=f_hat,
+            ctrl=ctrl,
+            f_jac=lambda xh, uk: jac(xh, uk),
+            stage_cost=stage_cost,
+            terminal_cost=terminal_cost,
+            stage_derivs=stage_derivs,
+            terminal_derivs=term_derivs,
+        )
+        assert X_hat.shape == (N + 1, 4) and U.shape == (N, 2)
+        u0 = U[0]
+        xs.append(x.cpu().numpy())
+        us.append(u0.cpu().numpy())
+        bs.append(float(b))
+        xn = f_hat(x_hat0, u0)
+        x, b = xn[:3], xn[3]
+        U_ws = torch.cat([U[1:], U[-1:]], dim=0)
+    g = golden("nominal_receding")
+    assert rel(np.array(xs), g["x_bar"]) < 1e-9
+    assert rel(np.array(us), g["u_bar"]) < 1e-9
+    assert rel(np.array(bs), g["b_real"]) < 1e-9
+    # the closures themselves evaluate on the device: cost and derivatives at the last plan's first point
+    J0 = stage_cost(X_hat[0], U[0], 0)
+    lx, lu, lxx, luu, lux = stage_derivs(X_hat[0], U[0], 0)
+    phi_x, phi_xx = term_derivs(X_hat[N])
+    assert torch.isfinite(J0) and lx.shape == (4,) and lu.shape == (2,) and phi_xx.shape == (4, 4)
+    assert float(phi_xx[3, 3]) == 2.0 * stage_cost.__self__.cost.qb
