@@ -78,7 +78,7 @@ class QuadraticClosures:
     -> (phi_x, phi_xx), stage_hess(x_hat, u, k) -> (l_xx, l_uu, l_ux), terminal_hess(x_hat_N) -> phi_xx.
     kind 'target' with wrap_angle is run_nominal.py:297-324 (the heading error wrapped, the derivatives taken
     at target_k = x_theta - wrap(x_theta - target_theta)); 'track' is core/tube_mpc.py:863-894 with X_ref
-    [N+1, >=3] / U_ref [N, 2] indexed by k.  The terminal derivatives include the barrier term 2 qb b
+    [N+1, >=3] / U_ref [N, 2] (or [B, N+1, >=3] / [B, N, 2]) indexed by k.  The terminal derivatives include the barrier term 2 qb b
     (run_nominal.py:321-323)."""
 
     def __init__(self, cost: QuadraticCost, X_ref: Optional[Tensor] = None, U_ref: Optional[Tensor] = None):
@@ -89,7 +89,8 @@ class QuadraticClosures:
     def _ref(self, x_hat: Tensor, k: Optional[int]) -> Tensor:
         c = self.cost
         if c.kind == "track":
-            r = self.X_ref[k if k is not None else -1][..., :3].to(x_hat)
+            kk = k if k is not None else -1
+            r = (self.X_ref[:, kk] if self.X_ref.ndim == 3 else self.X_ref[kk])[..., :3].to(x_hat)
             return r.expand(*x_hat.shape[:-1], 3)
         t = torch.tensor(c.target, dtype=x_hat.dtype, device=x_hat.device).expand(*x_hat.shape[:-1], 3)
         if not c.wrap_angle:
@@ -99,7 +100,8 @@ class QuadraticClosures:
 
     def _uref(self, u: Tensor, k: int) -> Tensor:
         if self.cost.kind == "track":
-            return self.U_ref[k].to(u).expand(*u.shape[:-1], 2)
+            r = self.U_ref[:, k] if self.U_ref.ndim == 3 else self.U_ref[k]
+            return r.to(u).expand(*u.shape[:-1], 2)
         return torch.zeros_like(u)
 
     def _err(self, x_hat: Tensor, k: Optional[int]) -> Tensor:
