@@ -623,10 +623,35 @@ __device__ __forceinline__ real barrier_at(const FP& p, real px, real py) {
   return vbarrier(p, h_sm<M>(p, px, py));
 }
 
-// _wrap_angle (run_nominal.py:32-34): atan2(sin e, cos e), evaluated as the generic kernels do (wrap_angle,
-// dtmpc_device.hpp)
-__device__ __forceinline__ real vwrap(real e) { return wrap_angle<real>(e); }
-__device__ __forceinline__ f2 vwrap(f2 e) { return f2{vwrap(e.x), vwrap(e.y)}; }
+// _wrap_angle (run_nominal.py:32-34): atan2(sin e, cos e) maps e to (-pi, pi].  The fused solver evaluates that
+// map directly, e - 2 pi rint(e / 2 pi) with 2 pi in two parts (the first product exact in the fma): < 1 ulp
+// from the exact wrap, where the reference's sin -> cos -> atan2 chain carries 2-3 ulp of its own, in 5
+// instructions instead of OCML's sin, cos and atan2 (~7 of them per step and iteration in the receding
+// solver).  The generic kernels keep atan2(sin, cos) (wrap_angle, dtmpc_device.hpp).  The one point where the
+// two maps part is e = +-pi itself (the reference's sign there is that of the rounded sin(pi)); the costs
+// square the wrapped error, so only a derivative at that exact point sees it.
+#if DTMPC_FAST_F64
+constexpr double k2PiA = 6.283185307179586, k2PiB = 2.4492935982947064e-16, k1o2Pi = 0.15915494309189535;
+#else
+constexpr float k2PiA = 6.28318548f, k2PiB = -1.74845553e-7f, k1o2Pi = 0.159154937f;
+#endif
+__device__ __forceinline__ real vrint(real x) {
+#if DTMPC_FAST_F64
+  return __builtin_rint(x);
+#else
+  return __builtin_rintf(x);
+#endif
+}
+__device__ __forceinline__ real vwrap(real e) {
+  DTMPC_NOCONTRACT
+  const real k = vrint(e * k1o2Pi);
+  return __builtin_elementwise_fma(-k, real(k2PiB), __builtin_elementwise_fma(-k, real(k2PiA), e));
+}
+__device__ __forceinline__ f2 vwrap(f2 e) {
+  DTMPC_NOCONTRACT
+  const f2 k = f2{vrint(e.x * k1o2Pi), vrint(e.y * k1o2Pi)};
+  return __builtin_elementwise_fma(-k, f2(k2PiB), __builtin_elementwise_fma(-k, f2(k2PiA), e));
+}
 
 // stage / terminal cost (stage_cost / term_cost, core/tube_mpc.py:823-842, 875-894): TRACK takes the
 // references r (state) and q (control), the nominal its fixed target (WRAP: heading error wrapped,
@@ -1479,7 +1504,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   f2 u0[NPR], u1[NPR];
   const int N1 = N - 1;
 #ifndef DTMPC_FAST_LS_LEAD4
-#define DTMPC_FAST_LS_LEAD4 0  // P = 4: step inputs in a ring of LEAD + 1 buffers refilled LEAD steps ahead (0: as P = 1)
+#define DTMPC_FAST_LS_LEAD4 4  // P = 4: step inputs in a ring of LEAD + 1 buffers refilled LEAD steps ahead (0: two buffers, as P = 1; B = 4,096: 2.13 ms at 0, 2.03 at 3, 2.01 at 4)
 #endif
   if (P == 4 && DTMPC_FAST_LS_LEAD4 > 0) {
     constexpr int LEAD = DTMPC_FAST_LS_LEAD4 > 0 ? DTMPC_FAST_LS_LEAD4 : 1, R = LEAD + 1;

@@ -34,6 +34,7 @@ for s in $STEPS; do
         run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf -s --timeout 300 --timeout-method thread
       fi ;;
     bench) run bench 900 python bench.py --steps 10 --warmup 3 ;;
+    b4096) run b4096 300 python bench.py --batch 4096 --steps 20 --warmup 8 --no-cpu --no-steady --no-extra ;;
     callers) run callers 600 python scripts/bench_callers.py --receding-only --f64 ;;
     bench_quick) run bench_quick 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-steady ;;
     *) echo "unknown step $s" ;;

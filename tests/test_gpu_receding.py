@@ -126,7 +126,8 @@ def test_receding_f32_failure_set_vs_oracle(dev, oracle_lib, monkeypatch):
     lies below the resolution of the large one, ~1e20), so the gains are rounding noise, and the antisymmetric
     part of V_xx that the reference's order leaves (core/ddp.py:252, never symmetrised) grows through the
     closed loop until it overflows: one step before the first non-finite gain Q_uu = [[2, 1.9e34],
-    [-1.9e34, 3e25]] (oracle, iteration 2 of the first solve).  Whether a run fails is therefore a property of
+    [-1.9e34, 3e25]] in one of them (oracle, second backward pass of the first solve); all 422 of the plain
+    build's failures are a non-finite Riccati step.  Whether a run fails is therefore a property of
     the evaluation order, not of the algorithm: liboracle_sym.so -- the plain build with V_xx mirrored from its
     upper triangle after every step, equal in exact arithmetic -- fails on ~0.5 % of the runs against ~10 % for
     the plain / fma / ulp builds, and the fused solver's order (csrc/dtmpc_fast.hip riccati_pk: fma chains,
@@ -236,7 +237,7 @@ def test_receding_fused_vs_generic(dev, oracle_lib, tag, monkeypatch):
     bl = [pair(runs[i], runs[j]) for i in range(2, 5) for j in range(i + 1, 5)]
     print(f"[receding fused vs generic {tag}] on {int(ok.sum())} runs: exits equal {dv[0]:.4f}, runs within {tol:g} "
           f"{dv[1]:.4f}; oracle builds pairwise {[(round(a, 4), round(b, 4)) for a, b in bl]}")
-    assert ok.mean() >= (1.0 if tag == "f64" else 0.8), ok.mean()
+    assert ok.mean() >= (1.0 if tag == "f64" else 0.7), ok.mean()  # f32: the builds fail on ~8 % each (union ~25 %)
     assert dv[0] >= min(b[0] for b in bl) - 0.03, (dv, bl)
     assert dv[1] >= min(b[1] for b in bl) - 0.05, (dv, bl)
 
