@@ -399,11 +399,12 @@ constexpr double kDS1 = -1.66666666666666324348e-01, kDS2 = 8.333333333322489461
 constexpr double kDC1 = 4.16666666666666019037e-02, kDC2 = -1.38888888888741095749e-03,
                  kDC3 = 2.48015872894767294178e-05, kDC4 = -2.75573143513906633035e-07,
                  kDC5 = 2.08757232129817482790e-09, kDC6 = -1.13596475577881948265e-11;
-// 1: OCML sincos out of line (the default); 0: inline in the cold branch -- measured WRONG results on the
-// one-lane f64 kernel (test_tube_step_fast64_vs_generic[1]: 5 % of trajectories within 1e-8; the two- and
-// four-lane forms and the out-of-line form are correct; the branch is never taken on those inputs, so the
-// inlined code changes the compilation, not the path -- kept for the record, never the default);
-// 2: none (ISA experiments only)
+// 1: OCML sincos out of line (the default); 0: inline in the cold branch; 2: none (ISA experiments only).
+// Round 3 measured wrong results with 0 on the one-lane f64 kernel (test_tube_step_fast64_vs_generic[1]);
+// on the round-4 source 0 and 1 are bitwise equal over two closed-loop steps (default contraction and
+// -ffp-contract=off alike) and 0 passes that test (profiles/r04/f64_far_sincos.txt).  The two sources differ
+// in the inline form's SGPR spilling (482 -> 403 spills to VGPR lanes in the cold-branch kernel), which is
+// where a compiler defect would sit; the round-3 build is not reproducible, so 1 stays the default.
 #ifndef DTMPC_FAST64_FAR
 #define DTMPC_FAST64_FAR 1
 #endif
