@@ -287,8 +287,14 @@ def ddp_sensitivity(*, problem: Optional[DubinsDBaSProblem] = None, cost: Option
         N = Vb.shape[1]
         r = resolve_sensitivity(f=f, f_jac=f_jac, ctrl=ctrl, stage_hess=stage_hess, terminal_hess=terminal_hess,
                                 horizon=N)
-        gX = torch.stack([upper_grad_x(Xb[:, k], k) for k in range(N)] + [upper_grad_xN(Xb[:, N])], 1)
-        gU = torch.stack([upper_grad_u(Vb[:, k], k) for k in range(N)], 1)
+        # the closures see what the reference hands them: one trajectory's row (x [4], u [2]) for an
+        # unbatched call, the batch's rows [B, 4] / [B, 2] otherwise
+        if single:
+            gX = torch.stack([upper_grad_x(X[k], k) for k in range(N)] + [upper_grad_xN(X[N])], 0)[None]
+            gU = torch.stack([upper_grad_u(V[k], k) for k in range(N)], 0)[None]
+        else:
+            gX = torch.stack([upper_grad_x(Xb[:, k], k) for k in range(N)] + [upper_grad_xN(Xb[:, N])], 1)
+            gU = torch.stack([upper_grad_u(Vb[:, k], k) for k in range(N)], 1)
         res = _ddp_sensitivity_upper(r.problem, r.cost, Xb, Vb, gX.to(Xb).expand(Xb.shape[0], N + 1, 4),
                                      gU.to(Xb).expand(Xb.shape[0], N, 2), want_lambda, check)
         if not single:
