@@ -605,8 +605,9 @@ __device__ __forceinline__ real h_grad(const FP& p, real px, real py, real& gx, 
 // b' = B(h(x')) - gamma (B(h(x)) - b) (core/barrier.py:75-108); Bc carries B(h(x))
 // G0 (gamma = 0): b' = B(h(x')) -- the general form adds (-0) * (B(h(x)) - b), which changes nothing
 // for finite values
-template <int M, bool G0 = false, class V>
-__device__ __forceinline__ void fhat(const FP& p, V& x0, V& x1, V& x2, V& b, V u0, V u1, V& Bc) {
+// the Dubins part alone (fhat's first half, operation for operation)
+template <class V>
+__device__ __forceinline__ void dubins(const FP& p, V& x0, V& x1, V& x2, V u0, V u1) {
   DTMPC_NOCONTRACT
   V sn, cs;
   vsincos(x2, sn, cs);
@@ -614,6 +615,11 @@ __device__ __forceinline__ void fhat(const FP& p, V& x0, V& x1, V& x2, V& b, V u
   x0 = ffma(dv, cs, x0);
   x1 = ffma(dv, sn, x1);
   x2 = ffma(V(p.dt), u1, x2);
+}
+template <int M, bool G0 = false, class V>
+__device__ __forceinline__ void fhat(const FP& p, V& x0, V& x1, V& x2, V& b, V u0, V u1, V& Bc) {
+  DTMPC_NOCONTRACT
+  dubins(p, x0, x1, x2, u0, u1);
   const V Bn = vbarrier(p, h_sm<M>(p, x0, x1));
   b = G0 ? Bn : ffma(V(-p.gamma), Bc - b, Bn);
   Bc = Bn;
@@ -741,7 +747,7 @@ struct StepIn {
   f2 kk;
 };
 
-template <bool TRACK, bool LOADX = true, class SV>
+template <bool TRACK, bool LOADX = true, class SV, bool LOADR = true>
 __device__ __forceinline__ void load_step(StepIn& L, const SV& S, int k) {
   if (LOADX) {
     const f4 X = S.x(k);
@@ -757,11 +763,15 @@ __device__ __forceinline__ void load_step(StepIn& L, const SV& S, int k) {
   L.V1 = V.y;
   S.G.template load<SV::g0>(S.r, k, L.Ka, L.Kb, L.kk);
   if (TRACK) {
-    const f4 R = S.xr(k);
+    if (LOADR) {
+      const f4 R = S.xr(k);
+      L.r0 = R.x;
+      L.r1 = R.y;
+      L.r2 = R.z;
+    } else {
+      L.r0 = L.r1 = L.r2 = 0.f;
+    }
     const f2 Q = S.ur(k);
-    L.r0 = R.x;
-    L.r1 = R.y;
-    L.r2 = R.z;
     L.q0 = Q.x;
     L.q1 = Q.y;
   } else {
@@ -1249,6 +1259,12 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
 // instructions in the kernel, 23 with two buffers)
 #define DTMPC_FAST_LS_DEPTH2 (DTMPC_FAST_F64 ? 0 : 1)
 #endif
+#ifndef DTMPC_FAST_LS_RECOMP
+// 1 (default): the line search re-rolls the tape's states (and the ancillary's reference states) from their
+// controls at gamma = 0 in f32 instead of reading them: -16 (nominal) / -32 (ancillary) B of reads per step,
+// bitwise the same tapes; same-box A/B (profiles/r04/ab_recompute.txt) time +-0, HBM traffic -15 %
+#define DTMPC_FAST_LS_RECOMP 1
+#endif
 template <int NPR>
 struct Cand {
   f2 a0[NPR], a1[NPR], a2[NPR], ab[NPR], Bp[NPR], J[NPR], al[NPR];
@@ -1523,25 +1539,54 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
       }
     }
   } else if (DTMPC_FAST_LS_DEPTH2) {
-  // four buffers in rotation, each refilled two steps before use
+  // four buffers in rotation, each refilled two steps before use.  RC (gamma = 0, f32): the current tape's
+  // states X_k -- and the ancillary's reference states -- are not read but re-rolled from their controls by
+  // the same Dubins arithmetic that produced them (init_tape / commit / the nominal's solve: rollout(x0, U)),
+  // so they are bit for bit the stored rows; their b is never needed (K's b column is zero at gamma = 0)
+  constexpr bool RC = DTMPC_FAST_LS_RECOMP && SV::g0 && !DTMPC_FAST_F64;
   auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
+  real o0 = x0[0], o1 = x0[1], o2 = x0[2], q0 = 0.f, q1 = 0.f, q2 = 0.f;
+  if (RC && TRACK) {
+    const f4 R0 = S.xr(0);
+    q0 = R0.x;
+    q1 = R0.y;
+    q2 = R0.z;
+  }
+  auto roll = [&](StepIn& L) {  // the tape's (and reference's) state of this step, then advance them
+    if (RC) {
+      L.X0 = o0;
+      L.X1 = o1;
+      L.X2 = o2;
+      dubins(p, o0, o1, o2, L.V0, L.V1);
+      if (TRACK) {
+        L.r0 = q0;
+        L.r1 = q1;
+        L.r2 = q2;
+        dubins(p, q0, q1, q2, L.q0, L.q1);
+      }
+    }
+  };
   StepIn A, Bs, Cs, Ds;
-  load_step<TRACK>(A, S, 0);
-  load_step<TRACK>(Bs, S, ix(1));
+  load_step<TRACK, !RC, SV, !RC>(A, S, 0);
+  load_step<TRACK, !RC, SV, !RC>(Bs, S, ix(1));
   for (int k = 0; k < N; k += 4) {
-    load_step<TRACK>(Cs, S, ix(k + 2));
+    load_step<TRACK, !RC, SV, !RC>(Cs, S, ix(k + 2));
+    roll(A);
     ls_step<TRACK, M, NPR, SV::g0>(p, c, A, C, u0, u1);
     keep(k, u0, u1);
     if (k + 1 >= N) break;
-    load_step<TRACK>(Ds, S, ix(k + 3));
+    load_step<TRACK, !RC, SV, !RC>(Ds, S, ix(k + 3));
+    roll(Bs);
     ls_step<TRACK, M, NPR, SV::g0>(p, c, Bs, C, u0, u1);
     keep(k + 1, u0, u1);
     if (k + 2 >= N) break;
-    load_step<TRACK>(A, S, ix(k + 4));
+    load_step<TRACK, !RC, SV, !RC>(A, S, ix(k + 4));
+    roll(Cs);
     ls_step<TRACK, M, NPR, SV::g0>(p, c, Cs, C, u0, u1);
     keep(k + 2, u0, u1);
     if (k + 3 >= N) break;
-    load_step<TRACK>(Bs, S, ix(k + 5));
+    load_step<TRACK, !RC, SV, !RC>(Bs, S, ix(k + 5));
+    roll(Ds);
     ls_step<TRACK, M, NPR, SV::g0>(p, c, Ds, C, u0, u1);
     keep(k + 3, u0, u1);
   }
@@ -1666,7 +1711,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
 #define DTMPC_FAST_CM_LEAD 2
 #endif
 #ifndef DTMPC_FAST_CM_RECOMP
-#define DTMPC_FAST_CM_RECOMP 0  // 1: the old tape's states are re-rolled from its controls, not read
+#define DTMPC_FAST_CM_RECOMP 1  // 1: the old tape's states are re-rolled from its controls, not read (CMR below)
 #endif
 // materialise the chosen candidate in place (commit_candidate): same arithmetic as its lane of the
 // line search; the old X[k+1] is read (prefetched) before it is overwritten
@@ -1675,26 +1720,22 @@ __device__ __forceinline__ void commit(const FP& p, real al, const real* x0, rea
   DTMPC_NOCONTRACT
   const int N = p.N;
   real s0 = x0[0], s1 = x0[1], s2 = x0[2], sb = x0[3], Bc = Bc0;
-#if DTMPC_FAST_CM_RECOMP
-  // the tape's X is rollout(x0, U) by this same scalar fhat (init_tape, commit), so re-rolling the old
-  // controls reproduces the old X bit for bit and saves its 16 B per step of HBM reads
-  real o0 = s0, o1 = s1, o2 = s2, ob = sb, Bo = Bc0;
-  constexpr bool LX = false;
-#else
-  constexpr bool LX = true;
-#endif
+  // CMR (gamma = 0, f32): the tape's X is rollout(x0, U) by this same scalar fhat (init_tape, commit), so
+  // re-rolling the old controls by its Dubins part reproduces the old x, y, theta bit for bit (b is never
+  // used: K's b column is zero) and saves 16 B per step of HBM reads.  (With gamma != 0 the re-roll would need
+  // the barrier too, measured slower in round 2; f64 is instruction-bound: both read the old states.)
+  constexpr bool CMR = DTMPC_FAST_CM_RECOMP && SV::g0 && !DTMPC_FAST_F64;
+  real o0 = s0, o1 = s1, o2 = s2;
+  constexpr bool LX = !CMR;
   Solve<false, SV::g0, SV::ric0, SV::lanes> T0;  // no references needed
   T0.r = S.r;
   T0.XA = S.XA;
   T0.UA = S.UA;
   T0.G = S.G;
   auto step = [&](const StepIn& cur, int k) {
-#if DTMPC_FAST_CM_RECOMP
-    const real e0 = s0 - o0, e1 = s1 - o1, e2 = s2 - o2, e3 = sb - ob;
-    fhat<M>(p, o0, o1, o2, ob, cur.V0, cur.V1, Bo);
-#else
-    const real e0 = s0 - cur.X0, e1 = s1 - cur.X1, e2 = s2 - cur.X2, e3 = sb - cur.X3;
-#endif
+    const real e0 = s0 - (CMR ? o0 : cur.X0), e1 = s1 - (CMR ? o1 : cur.X1), e2 = s2 - (CMR ? o2 : cur.X2);
+    const real e3 = sb - cur.X3;  // CMR: unused (kdot<g0> drops the b column)
+    if (CMR) dubins(p, o0, o1, o2, cur.V0, cur.V1);
 #if DTMPC_FAST_KFMA
     const real du0 = cur.kk.x + kdot<SV::g0>(cur.Ka, e0, e1, e2, e3);
     const real du1 = cur.kk.y + kdot<SV::g0>(cur.Kb, e0, e1, e2, e3);
