@@ -247,6 +247,7 @@ def test_ilqr_batched_vs_oracle(dev, oracle_lib, tag, variant, monkeypatch):
 # the builds themselves split from each other by more than ties (the 20-iteration tracking solve from perturbed
 # starts: chaotic from the first iteration), on >= the builds' own pass rate under the same rule - 2 points.
 F32_TRUTH_GATE = 1.0
+F32_THETA_DRIFT = 5e-2  # f32 vs f64 free-running theta, relative, any step of 20 (provisional: calibrating)
 TIE_GATE = 0.99
 
 
@@ -646,11 +647,23 @@ def test_free_running_loop_f32_theta_bounded(dev):
         thetas.append(m.theta.double().cpu().numpy())
         healthy.append(m.healthy_count / B)
     thetas = np.array(thetas)
-    print(f"[free-running f32 B={B}] theta after 20 steps {thetas[-1].round(4).tolist()}, "
-          f"max |theta| {np.abs(thetas).max():.4g}, healthy fraction min {min(healthy):.5f}")
+    # the same loop in f64 (the reference's configured precision) under the same health policy: the f32
+    # batch-mean update must track it step by step
+    m64 = TubeMPC(st, batch=B, device=dev, dtype=torch.float64, disturbance="philox", seed=0, grad_bound=m.cfg.grad_bound)
+    m64.reset(x0.double())
+    th64 = []
+    for _ in range(20):
+        m64.step()
+        th64.append(m64.theta.cpu().numpy())
+    th64 = np.array(th64)
+    drift = np.abs(thetas - th64) / np.maximum(np.abs(th64), 1e-3)
+    print(f"[free-running f32 B={B}] theta after 20 steps {thetas[-1].round(4).tolist()} (f64 loop "
+          f"{th64[-1].round(4).tolist()}), max |theta| {np.abs(thetas).max():.4g}, healthy fraction min "
+          f"{min(healthy):.5f}; relative theta drift from the f64 loop per step (max over components) "
+          f"{[float(f'{v:.2g}') for v in drift.max(1)]}")
     assert np.isfinite(thetas).all()
-    assert np.abs(thetas).max() < 1e3, thetas.max(0)
     assert min(healthy) > 0.97, healthy
+    assert drift.max() <= F32_THETA_DRIFT, drift.max(1)
 
 
 def test_run_closed_loop_experiment_outputs(dev, tmp_path):
