@@ -247,7 +247,6 @@ def test_ilqr_batched_vs_oracle(dev, oracle_lib, tag, variant, monkeypatch):
 # the builds themselves split from each other by more than ties (the 20-iteration tracking solve from perturbed
 # starts: chaotic from the first iteration), on >= the builds' own pass rate under the same rule - 2 points.
 F32_TRUTH_GATE = 1.0
-F32_THETA_DRIFT = 5e-2  # f32 vs f64 free-running theta, relative, any step of 20 (provisional: calibrating)
 TIE_GATE = 0.99
 
 
@@ -623,7 +622,7 @@ def test_closed_loop_vs_reference_loop_f32_health_policy(dev):
     assert rel(th[:, 5], g["qba_history"]) < t
 
 
-def test_free_running_loop_f32_theta_bounded(dev):
+def test_free_running_loop_f32_theta_bounded(dev, monkeypatch):
     """The steady-state workload of bench.py: B = 65,536 f32, fixed iterations, 20 free-running closed-loop
     steps (warm-started, theta updated every step under the f32 health policy) keep theta finite and
     bounded and nearly every trajectory healthy (measured: ~98.5 % per step; the rest are flagged or
@@ -647,23 +646,35 @@ def test_free_running_loop_f32_theta_bounded(dev):
         thetas.append(m.theta.double().cpu().numpy())
         healthy.append(m.healthy_count / B)
     thetas = np.array(thetas)
-    # the same loop in f64 (the reference's configured precision) under the same health policy: the f32
-    # batch-mean update must track it step by step
-    m64 = TubeMPC(st, batch=B, device=dev, dtype=torch.float64, disturbance="philox", seed=0, grad_bound=m.cfg.grad_bound)
-    m64.reset(x0.double())
-    th64 = []
-    for _ in range(20):
-        m64.step()
-        th64.append(m64.theta.cpu().numpy())
-    th64 = np.array(th64)
-    drift = np.abs(thetas - th64) / np.maximum(np.abs(th64), 1e-3)
+    # the same loop in f64 (the reference's configured precision) under the same health policy, on the fused
+    # f64 kernel and on the generic one (DTMPC_FAST64=0: a second f64 rounding of the same algorithm).  The
+    # shared theta is a batch mean dominated by the few obstacle-grazing trajectories' large gradients, so
+    # after a few steps it is as sensitive to rounding as they are: the f32 loop must track f64 as closely
+    # as the two f64 evaluations track each other
+    def loop64(fast):
+        monkeypatch.setenv("DTMPC_FAST64", fast)
+        m64 = TubeMPC(st, batch=B, device=dev, dtype=torch.float64, disturbance="philox", seed=0,
+                      grad_bound=m.cfg.grad_bound)
+        m64.reset(x0.double())
+        out = []
+        for _ in range(20):
+            m64.step()
+            out.append(m64.theta.cpu().numpy())
+        return np.array(out)
+
+    th64, th64g = loop64("1"), loop64("0")
+    monkeypatch.delenv("DTMPC_FAST64")
+    rel_d = lambda a, b: (np.abs(a - b) / np.maximum(np.abs(b), 1e-3)).max(1)  # noqa: E731
+    d32, d64 = rel_d(thetas, th64), rel_d(th64g, th64)
     print(f"[free-running f32 B={B}] theta after 20 steps {thetas[-1].round(4).tolist()} (f64 loop "
-          f"{th64[-1].round(4).tolist()}), max |theta| {np.abs(thetas).max():.4g}, healthy fraction min "
-          f"{min(healthy):.5f}; relative theta drift from the f64 loop per step (max over components) "
-          f"{[float(f'{v:.2g}') for v in drift.max(1)]}")
-    assert np.isfinite(thetas).all()
+          f"{th64[-1].round(4).tolist()}, generic f64 {th64g[-1].round(4).tolist()}), max |theta| "
+          f"{np.abs(thetas).max():.4g}, healthy fraction min {min(healthy):.5f}; relative theta distance per step "
+          f"f32 vs f64 {[float(f'{v:.2g}') for v in d32]}, f64 generic vs fused {[float(f'{v:.2g}') for v in d64]}")
+    assert np.isfinite(thetas).all() and np.abs(thetas).max() < 1e2, thetas.max(0)
     assert min(healthy) > 0.97, healthy
-    assert drift.max() <= F32_THETA_DRIFT, drift.max(1)
+    assert d32[0] <= 1e-3, d32  # one step: the batch-mean update of the same theta0
+    # later steps: no further from f64 than f64's two roundings are from each other (x 10), or 1e-2
+    assert np.all(d32 <= np.maximum(10.0 * np.maximum.accumulate(d64), 1e-2)), (d32, d64)
 
 
 def test_run_closed_loop_experiment_outputs(dev, tmp_path):
