@@ -238,3 +238,22 @@ def test_nominal_receding_vs_run_nominal(oracle_lib):
         U = np.concatenate([V[:, 1:], V[:, -1:]], axis=1)
     assert rel(np.array(xs), g["x_bar"]) < 1e-9
     assert rel(np.array(us), g["u_bar"]) < 1e-9
+
+
+def test_symmetric_vxx_build_is_the_same_algorithm(oracle_lib):
+    """liboracle_sym.so (V_xx mirrored from its upper triangle after every Riccati step; the receding f32
+    failure-set test's fourth rounding) solves the reference's golden nominal iLQR cases like the plain build:
+    f64, well-conditioned cases, within the golden tolerance -- it is a rounding of the same recursion."""
+    g = golden("ilqr_f64")
+    st = paper_setup()
+    sp, cn = st.problem.to_c(), st.nominal_cost.to_c()
+    outs = [oracle_lib.Oracle(np.float64, variant=v).ilqr_solve(sp, cn, ilqr_cfg(10, 1e-3).to_c(), g["x0"],
+                                                                 g["Vinit_nom"]) for v in ("plain", "sym")]
+    n = 0
+    for i in range(g["x0"].shape[0]):
+        if not np.isfinite(g["X_nom"][i]).all() or g["cond_nom"][i] > CHAOTIC:
+            continue
+        t = tol_for(np.float64, g["cond_nom"][i])
+        assert rel(outs[1][0][i], outs[0][0][i]) < t and rel(outs[1][0][i], g["X_nom"][i]) < t, i
+        n += 1
+    assert n >= 5
