@@ -28,6 +28,7 @@ from __future__ import annotations
 import argparse
 import glob
 import json
+import math
 import os
 import re
 import sys
@@ -282,6 +283,37 @@ def tube_leg(dev, dtype_name: str, B: int, steps: int, warmup: int, adapt: bool 
     return out
 
 
+def receding_leg(dev, dtype_name: str, B: int = 65536, H: int = 20, reps: int = 3):
+    """The receding-horizon nominal MPC (run_nominal.py:204-415, BASELINE config 1's workload) batched over B
+    starts x0 ~ U[0,1]^2 x U[0, pi/2] (paper configuration, tol = 1e-3, early exits): one dtmpc_nominal_receding
+    launch runs every run's whole loop (the fused solver, csrc/dtmpc_fast.hip receding_fast_kernel).  Time per
+    receding step = launch time / H; iLQR solves/s = the steps the runs actually took / launch time."""
+    from diff_tube_mpc_strict_pt.core.problem import paper_config
+    from diff_tube_mpc_strict_pt.core.receding import nominal_receding, receding_setup_from_config
+
+    tdt = torch.float32 if dtype_name == "f32" else torch.float64
+    problem, cost, icfg = receding_setup_from_config(paper_config())
+    g = torch.Generator().manual_seed(0)
+    u = torch.rand(B, 3, generator=g, dtype=torch.float64)
+    x0 = torch.stack([u[:, 0], u[:, 1], u[:, 2] * (math.pi / 2)], 1).to(tdt).to(dev)
+    nominal_receding(problem=problem, cost=cost, cfg=icfg, x0=x0[:1024], H=2, check=False)
+    ms, r = [], None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        e0.record()
+        r = nominal_receding(problem=problem, cost=cost, cfg=icfg, x0=x0, H=H, check=False)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        ms.append(e0.elapsed_time(e1))
+    t = float(np.median(ms))
+    solves = int(r.h_ran.sum())
+    return {"workload": "receding-horizon nominal MPC (run_nominal.py), B runs x H steps, tol=1e-3, 7 alphas",
+            "batch": B, "H": H, "dtype": dtype_name, "ms_per_receding_step": t / H, "launch_ms": t,
+            "ilqr_solves_per_s": solves / (t * 1e-3), "solves": solves, "failed": int((r.status != 0).sum()),
+            "success": int((r.success_t >= 0).sum()), "collided": int(r.collided.sum())}
+
+
 def _free_port() -> int:
     import socket
 
@@ -503,6 +535,7 @@ def main() -> None:
                               for d in ("f32", "f64")}
         out["nominal_ddp"]["f32_generic"] = nominal_ddp_leg(dev, "f32", B=4096, steps=args.steps,
                                                             warmup=args.warmup, generic=True)
+        out["receding"] = {d: receding_leg(dev, d) for d in ("f32", "f64")}
     if args.dry_run:
         out["dry_run"] = True
     if rank == 0 and not args.no_cpu and world == 1 and not args.dry_run:
