@@ -102,3 +102,29 @@ def test_rollout_and_point_closures(dev):
     lx, lu, *_ = q1.stage_derivs(xh, u0, 0)
     assert abs(float(lx[2]) - 0.2) <= 1e-12 and abs(float(lx[0])) <= 1e-12
     assert abs(float(q1.stage_cost(xh, u0, 0)) - 0.01) <= 1e-12
+
+
+def test_ilqr_keyword_form_batched_vs_typed(dev):
+    """The keyword form with a batch (x0 [B, 4], V_init [B, N, 2]) returns the typed call's X*, V* bit for bit
+    (the same kernel); ctrl=None is the unclamped box."""
+    import dataclasses
+
+    from diff_tube_mpc_strict_pt.core import ilqr_solve
+
+    cl, x0, X, V = _setup(dev)
+    icfg = cl["ilqr_cfg"]
+    B = 5
+    xb = x0[None].repeat(B, 1)
+    xb[:, 0] += torch.linspace(0.0, 0.2, B, dtype=xb.dtype, device=dev)
+    Ub = torch.zeros(B, icfg.horizon, 2, dtype=xb.dtype, device=dev)
+    Ub[:, :, 0] = 10.0
+    kw = dict(cfg=icfg, f=cl["f_hat"], f_jac=cl["f_jac"], stage_cost=cl["stage_cost"],
+              terminal_cost=cl["terminal_cost"], stage_derivs=cl["stage_derivs"], terminal_derivs=cl["term_derivs"])
+    Xk, Vk = ilqr_solve(x0=xb, V_init=Ub, ctrl=cl["ctrl"], **kw)
+    qc = cl["stage_cost"].__self__
+    r = ilqr_solve(problem=dataclass_problem(cl), cost=qc.cost, cfg=icfg, x0=xb, V_init=Ub)
+    assert torch.equal(Xk, r.X) and torch.equal(Vk, r.V)
+    Xn, Vn = ilqr_solve(x0=xb, V_init=Ub, ctrl=None, **kw)
+    p_unb = dataclasses.replace(cl["f_hat"].problem, u_min=(-np.inf, -np.inf), u_max=(np.inf, np.inf))
+    r2 = ilqr_solve(problem=p_unb, cost=qc.cost, cfg=icfg, x0=xb, V_init=Ub)
+    assert torch.isfinite(Xn).all() and torch.equal(Xn, r2.X) and torch.equal(Vn, r2.V)
