@@ -38,8 +38,8 @@ from torch import Tensor
 from .control import BoxClampControl
 from .problem import DubinsDBaSProblem, ILQRConfig, QuadraticCost
 
-__all__ = ["DBaSDynamics", "QuadraticClosures", "nominal_closures", "resolve_ilqr", "resolve_sensitivity",
-           "ResolvedCall"]
+__all__ = ["DBaSDynamics", "QuadraticClosures", "ParamClosures", "nominal_closures", "resolve_ilqr",
+           "resolve_sensitivity", "resolve_ift", "ResolvedCall"]
 
 
 def _wrap(e: Tensor) -> Tensor:
@@ -173,6 +173,94 @@ def nominal_closures(cfg: Dict[str, Any]) -> Dict[str, Any]:
             "ctrl": BoxClampControl(u_min=problem.u_min, u_max=problem.u_max, active_tol=problem.active_tol),
             "stage_cost": qc.stage_cost, "terminal_cost": qc.terminal_cost, "stage_derivs": qc.stage_derivs,
             "term_derivs": qc.terminal_derivs, "ilqr_cfg": icfg}
+
+
+class ParamClosures:
+    """The general path's gradient closures over raw parameters, for ift_gradient's keyword form
+    (core/ift.py:35-43): the ancillary set of core/tube_mpc.py:469-489 (f_hat_aux_grad, stage_cost_aux_grad,
+    terminal_cost_aux_grad over theta = AuxiliaryTheta and the reference tensors X_ref [N+1, 3] / U_ref
+    [N, 2]) or, with ``target``, the nominal set of :556-585 over theta-bar = NominalTheta (with the
+    tightening s).  ``f`` / ``stage_cost`` / ``terminal_cost`` have the reference's signatures and evaluate
+    on the device with the parameters' current values (weights softplus(raw), alpha = softplus + 1e-6,
+    gamma = tanh, core/params.py); the nominal ``f`` with a tightening s != 0 is not evaluated point-wise
+    (its h - s lives in the fused kernels only)."""
+
+    def __init__(self, problem: DubinsDBaSProblem, theta, *, X_ref: Optional[Tensor] = None,
+                 U_ref: Optional[Tensor] = None, target: Optional[Tuple[float, float, float]] = None):
+        if (X_ref is None) == (target is None):
+            raise ValueError("pass X_ref / U_ref (the ancillary set) or target (the nominal set)")
+        if X_ref is not None and U_ref is None:
+            raise ValueError("the ancillary set needs X_ref and U_ref")
+        self.problem, self.theta, self.X_ref, self.U_ref, self.target = problem, theta, X_ref, U_ref, target
+
+    @property
+    def nominal(self) -> bool:
+        return self.target is not None
+
+    def cost(self) -> QuadraticCost:
+        return (QuadraticCost(kind="target", target=tuple(float(v) for v in self.target)) if self.nominal
+                else QuadraticCost(kind="track"))
+
+    def f(self, x_hat: Tensor, u: Tensor) -> Tensor:
+        th = self.theta
+        if self.nominal and float(th.tight()) != 0.0:
+            raise NotImplementedError("point-wise f with the tightening h - s: use the typed general step")
+        p = dataclasses.replace(self.problem, dbas_alpha=float(th.alpha()), dbas_gamma=float(th.gamma()))
+        return DBaSDynamics(p)(x_hat, u)
+
+    def _w(self, t: Tensor, like: Tensor) -> Tensor:
+        return t.detach().to(dtype=like.dtype, device=like.device)
+
+    def stage_cost(self, x_hat: Tensor, u: Tensor, k: int) -> Tensor:
+        from . import _points as P
+
+        P.require_device(x_hat, u)
+        th = self.theta
+        ref = (torch.tensor(self.target, dtype=x_hat.dtype, device=x_hat.device) if self.nominal
+               else self.X_ref[k][..., :3].to(x_hat))
+        dx = x_hat[..., :3] - ref
+        du = u if self.nominal else u - self.U_ref[k].to(u)
+        b = x_hat[..., 3]
+        return ((self._w(th.Q(), x_hat) * dx * dx).sum(-1) + (self._w(th.R(), x_hat) * du * du).sum(-1)
+                + self._w(th.qb(), x_hat) * (b * b))
+
+    def terminal_cost(self, x_hat_N: Tensor) -> Tensor:
+        from . import _points as P
+
+        P.require_device(x_hat_N)
+        th = self.theta
+        ref = (torch.tensor(self.target, dtype=x_hat_N.dtype, device=x_hat_N.device) if self.nominal
+               else self.X_ref[-1][..., :3].to(x_hat_N))
+        dx = x_hat_N[..., :3] - ref
+        b = x_hat_N[..., 3]
+        return (self._w(th.Qf(), x_hat_N) * dx * dx).sum(-1) + self._w(th.qb(), x_hat_N) * (b * b)
+
+
+def resolve_ift(*, theta_tensors, xi_fn, f_fn, stage_cost_fn, terminal_cost_fn) -> Tuple[ParamClosures, list]:
+    """The keyword form of ift_gradient (core/ift.py:35-43) -> its closures' carrier and, per requested tensor,
+    where its gradient sits: ("theta", index into IFTGradient.split()) or ("X_ref" | "U_ref", None)."""
+    owners = {n: _owner(fn, ParamClosures, n) for n, fn in
+              (("f_fn", f_fn), ("stage_cost_fn", stage_cost_fn), ("terminal_cost_fn", terminal_cost_fn))}
+    pc = owners["f_fn"]
+    if any(o is not pc for o in owners.values()):
+        raise ValueError("f_fn, stage_cost_fn and terminal_cost_fn come from different ParamClosures")
+    xi = xi_fn() if xi_fn is not None else None
+    if xi is not None and isinstance(xi, Tensor) and xi.requires_grad:
+        raise NotImplementedError("xi_fn must return a detached x_hat0 (the reference's callers pass "
+                                  "x_hat0.detach(): xi contributes nothing)")
+    params = pc.theta.tensors()
+    where = []
+    for t in theta_tensors:
+        hit = [i for i, q in enumerate(params) if q is t]
+        if hit:
+            where.append(("theta", hit[0]))
+        elif pc.X_ref is not None and t is pc.X_ref:
+            where.append(("X_ref", None))
+        elif pc.U_ref is not None and t is pc.U_ref:
+            where.append(("U_ref", None))
+        else:
+            raise ValueError("theta_tensors holds a tensor the closures do not depend on")
+    return pc, where
 
 
 @dataclasses.dataclass(frozen=True)

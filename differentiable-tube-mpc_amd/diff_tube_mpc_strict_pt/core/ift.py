@@ -13,6 +13,7 @@ oracle/oracle_general.h); xi = x_hat0.detach() contributes nothing, as in the re
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -53,15 +54,50 @@ class IFTGradient:
         return [t[:, 0:3], t[:, 3:5], t[:, 5:8], t[:, 8], t[:, 9], t[:, 10], t[:, 11]]
 
 
-def ift_gradient(*, inputs: IFTInputs, problem: DubinsDBaSProblem, cost: QuadraticCost,
-                 theta_raw: Sequence[float] | Tensor, X_ref: Optional[Tensor] = None,
-                 U_ref: Optional[Tensor] = None) -> IFTGradient:
+def ift_gradient(*, inputs: IFTInputs, problem: Optional[DubinsDBaSProblem] = None,
+                 cost: Optional[QuadraticCost] = None, theta_raw: Sequence[float] | Tensor | None = None,
+                 X_ref: Optional[Tensor] = None, U_ref: Optional[Tensor] = None, theta_tensors=None, xi_fn=None,
+                 f_fn=None, stage_cost_fn=None, terminal_cost_fn=None):
     """ift_gradient (core/ift.py:35-92).
+
+    The reference's keyword form -- ift_gradient(inputs=, theta_tensors=, xi_fn=, f_fn=, stage_cost_fn=,
+    terminal_cost_fn=) with the closures of one core.closures.ParamClosures and unbatched inputs -- is resolved
+    to this typed call and returns the reference's list: one gradient per tensor of theta_tensors, shaped like
+    it (the raw parameters of the closures' theta, and the ancillary set's X_ref / U_ref).
 
     cost.kind 'track' = the ancillary closures (core/tube_mpc.py:461-500; also returns dL/dX_ref,
     dL/dU_ref), 'target' = the nominal ones (:556-585, with the tightening).  Weights and the DBaS
     alpha / gamma / tightening come from ``theta_raw`` [12] through core/params.py; ``cost`` supplies
     the kind and target, ``problem`` the system, obstacles, barrier type and eps."""
+    if f_fn is not None:
+        if problem is not None or cost is not None or theta_raw is not None:
+            raise TypeError("pass either problem / cost / theta_raw (typed form) or the closures, not both")
+        from .closures import resolve_ift
+
+        pc, where = resolve_ift(theta_tensors=theta_tensors, xi_fn=xi_fn, f_fn=f_fn, stage_cost_fn=stage_cost_fn,
+                                terminal_cost_fn=terminal_cost_fn)
+        single = inputs.X.ndim == 2
+        up = (lambda t: t[None]) if single else (lambda t: t)  # noqa: E731
+        inb = IFTInputs(X=up(inputs.X), V=up(inputs.V), delta_X=up(inputs.delta_X), delta_V=up(inputs.delta_V),
+                        delta_lambda=up(inputs.delta_lambda))
+        Bn = inb.X.shape[0]
+        Xr = Ur = None
+        if not pc.nominal:
+            Xr = pc.X_ref.detach()
+            Ur = pc.U_ref.detach()
+            Xr = (Xr[None].expand(Bn, *Xr.shape) if Xr.ndim == 2 else Xr).to(inb.X)
+            Ur = (Ur[None].expand(Bn, *Ur.shape) if Ur.ndim == 2 else Ur).to(inb.X)
+        g = ift_gradient(inputs=inb, problem=dataclasses.replace(pc.problem, horizon=inb.V.shape[1]),
+                         cost=pc.cost(), theta_raw=pc.theta.raw(), X_ref=Xr, U_ref=Ur)
+        parts = g.split()
+        out = []
+        for t, (kind, i) in zip(theta_tensors, where):
+            v = parts[i] if kind == "theta" else (g.X_ref if kind == "X_ref" else g.U_ref)
+            v = v[0] if single else v
+            out.append(v.reshape(t.shape).to(dtype=t.dtype))
+        return out
+    if problem is None or cost is None or theta_raw is None:
+        raise TypeError("ift_gradient needs problem, cost and theta_raw (typed form) or the closures (keyword form)")
     X, V = inputs.X, inputs.V
     _require_device(X, V, inputs.delta_X, inputs.delta_V, inputs.delta_lambda, X_ref, U_ref)
     B, N = X.shape[0], problem.horizon

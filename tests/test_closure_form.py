@@ -101,3 +101,42 @@ def test_keyword_form_refusals():
     # the closures' own evaluation is device-only too
     with pytest.raises(ValueError, match="device tensors"):
         cl["stage_cost"](torch.zeros(4, dtype=torch.float64), torch.zeros(2, dtype=torch.float64), 0)
+
+
+def test_ift_keyword_form_resolution():
+    """ift_gradient(inputs=, theta_tensors=, xi_fn=, f_fn=, stage_cost_fn=, terminal_cost_fn=) (core/ift.py:35-43):
+    the closures of one ParamClosures resolve, theta_tensors map by identity onto the raw parameters and the
+    reference tensors; a foreign tensor, mixed closure sets, a xi that needs gradients, or a mix with the typed
+    arguments are refused; the call reaches dispatch and refuses host tensors."""
+    from diff_tube_mpc_strict_pt.core import IFTInputs, ift_gradient
+    from diff_tube_mpc_strict_pt.core.closures import ParamClosures, resolve_ift
+    from diff_tube_mpc_strict_pt.core.params import theta_from_raw
+    from diff_tube_mpc_strict_pt.core.problem import DubinsDBaSProblem
+
+    N = 6
+    prob = DubinsDBaSProblem(horizon=N)
+    th = theta_from_raw(np.linspace(-0.5, 0.5, 12), False)
+    Xr, Ur = torch.zeros(N + 1, 3, dtype=torch.float64), torch.zeros(N, 2, dtype=torch.float64)
+    pc = ParamClosures(prob, th, X_ref=Xr, U_ref=Ur)
+    x0 = torch.zeros(4, dtype=torch.float64)
+    kw = dict(xi_fn=lambda: x0, f_fn=pc.f, stage_cost_fn=pc.stage_cost, terminal_cost_fn=pc.terminal_cost)
+    got, where = resolve_ift(theta_tensors=th.tensors() + [Xr, Ur], **kw)
+    assert got is pc and where == [("theta", i) for i in range(6)] + [("X_ref", None), ("U_ref", None)]
+    with pytest.raises(ValueError, match="do not depend"):
+        resolve_ift(theta_tensors=[torch.zeros(3)], **kw)
+    other = ParamClosures(prob, th, target=(1.0, 1.0, 0.0))
+    with pytest.raises(ValueError, match="different"):
+        resolve_ift(theta_tensors=th.tensors(), **{**kw, "terminal_cost_fn": other.terminal_cost})
+    with pytest.raises(NotImplementedError, match="detached"):
+        resolve_ift(theta_tensors=th.tensors(), **{**kw, "xi_fn": lambda: x0.clone().requires_grad_(True)})
+    with pytest.raises(TypeError, match="arbitrary Python closure"):
+        resolve_ift(theta_tensors=th.tensors(), **{**kw, "f_fn": lambda x, u: x})
+    with pytest.raises(ValueError, match="X_ref / U_ref"):
+        ParamClosures(prob, th)
+    inp = IFTInputs(X=torch.zeros(N + 1, 4, dtype=torch.float64), V=torch.zeros(N, 2, dtype=torch.float64),
+                    delta_X=torch.zeros(N + 1, 4, dtype=torch.float64), delta_V=torch.zeros(N, 2, dtype=torch.float64),
+                    delta_lambda=torch.zeros(N + 1, 4, dtype=torch.float64))
+    with pytest.raises(TypeError, match="not both"):
+        ift_gradient(inputs=inp, problem=prob, theta_tensors=th.tensors(), **kw)
+    with pytest.raises(ValueError, match="device tensors"):
+        ift_gradient(inputs=inp, theta_tensors=th.tensors(), **kw)

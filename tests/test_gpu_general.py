@@ -250,3 +250,39 @@ def test_run_closed_loop_experiment_general_outputs(dev, tmp_path):
     assert set(res["summary"]) == {"system", "H", "N", "final_state", "final_barrier_state", "final_loss"}
     g = golden("general_A_f64")
     assert abs(np.load(os.path.join(tmp_path, "loss.npy"))[0] - g["loss"][0]) < 1e-9  # step 0 has no disturbance
+
+
+def test_ift_gradient_keyword_form_vs_reference_kats(dev):
+    """ift_gradient in the reference's keyword form (core/ift.py:35-43): closures from core.closures.ParamClosures
+    over the raw parameter tensors (and the ancillary set's X_ref / U_ref tensors), unbatched IFTInputs, a
+    detached xi -- on the reference's own ift_gradient KATs, the same figures as the typed call."""
+    from diff_tube_mpc_strict_pt.core import IFTInputs, ift_gradient
+    from diff_tube_mpc_strict_pt.core.closures import ParamClosures
+    from diff_tube_mpc_strict_pt.core.params import theta_from_raw
+    from diff_tube_mpc_strict_pt.core.problem import general_setup_from_config
+
+    k = golden("ift_general_f64")
+    base = general_setup_from_config(general_cfg())
+    n, N = k["X"].shape[0], k["X"].shape[1] - 1
+    T = torch.float64
+    for c in range(n):
+        prob = dataclasses.replace(base.problem, horizon=N, barrier_type="log" if int(k["btype"][c]) else "inverse")
+        inp = IFTInputs(X=_t(k["X"][c], T, dev), V=_t(k["V"][c], T, dev), delta_X=_t(k["dX"][c], T, dev),
+                        delta_V=_t(k["dV"][c], T, dev), delta_lambda=_t(k["dlam"][c], T, dev))
+        x0 = inp.X[0].clone()
+        th = theta_from_raw(np.concatenate([k["raw_aux"][c], [0.0]]), False, dtype=T, device=dev)
+        Xr, Ur = _t(k["Xref"][c], T, dev), _t(k["Uref"][c], T, dev)
+        pc = ParamClosures(prob, th, X_ref=Xr, U_ref=Ur)
+        g = ift_gradient(inputs=inp, theta_tensors=th.tensors() + [Xr, Ur], xi_fn=lambda: x0.detach(), f_fn=pc.f,
+                         stage_cost_fn=pc.stage_cost, terminal_cost_fn=pc.terminal_cost)
+        assert [tuple(a.shape) for a in g] == [tuple(t.shape) for t in th.tensors() + [Xr, Ur]]
+        flat = torch.cat([a.reshape(-1) for a in g[:6]]).cpu().numpy()
+        ref = k["g_aux"][c]
+        assert close(flat, ref[:11], 1e-9, 1e-10), c
+        assert close(g[6].cpu().numpy().reshape(-1), ref[11:11 + 3 * (N + 1)], 1e-12, 1e-13), c
+        assert close(g[7].cpu().numpy().reshape(-1), ref[11 + 3 * (N + 1):], 1e-12, 1e-13), c
+        thn = theta_from_raw(k["raw_nom"][c], True, dtype=T, device=dev)
+        pn = ParamClosures(prob, thn, target=base.target)
+        gn = ift_gradient(inputs=inp, theta_tensors=thn.tensors(), xi_fn=lambda: x0.detach(), f_fn=pn.f,
+                          stage_cost_fn=pn.stage_cost, terminal_cost_fn=pn.terminal_cost)
+        assert close(torch.cat([a.reshape(-1) for a in gn]).cpu().numpy(), k["g_nom"][c], 1e-9, 1e-10), c
