@@ -2101,10 +2101,15 @@ __device__ __forceinline__ const char* kargs_ws() { return (const char*)kargs()-
 #define DTMPC_FAST_PIN 1
 #endif
 // the problem constants of one phase; the obstacle table pinned in VGPRs (every candidate of every
-// step reads it; in scalar registers it is what the compiler would spill first)
+// step reads it; in scalar registers it is what the compiler would spill first).  f64 pins at most five
+// obstacles (30 VGPRs; the paper's M = 5): the f64 receding kernel at M = 8 with its 48-VGPR table spilled
+// into scratch inside its per-lane divergent loops and returned run-to-run different results (NaN on one
+// box, 55 % of the runs off on another; unchanged by -ftrivial-auto-var-init, gone with the table
+// unpinned -- DESIGN.md section 9, profiles/r04/m8_receding.txt); f64 at M = 5 runs 13.6 ms pinned, 15.6 unpinned.
 template <int M>
 __device__ __forceinline__ FP pin_p(FP p) {
 #if DTMPC_FAST_PIN
+  if (DTMPC_FAST_F64 && Obs<M>::n > 5) return p;
 #pragma unroll
   for (int j = 0; j < Obs<M>::n; ++j) {
     real vx = p.cx[j], vy = p.cy[j], vr = p.r2[j];

@@ -36,6 +36,10 @@ for s in $STEPS; do
     bench) run bench 900 python bench.py --steps 10 --warmup 3 ;;
     b4096) run b4096 300 python bench.py --batch 4096 --steps 20 --warmup 8 --no-cpu --no-steady --no-extra ;;
     callers) run callers 600 python scripts/bench_callers.py --receding-only --f64 ;;
+    f64lanes)  # the lane rule re-checked on the f64 fused kernel (DTMPC_TUBE_LANES forces the count)
+      for b in 65536 16384; do for l in 1 2 4; do
+        DTMPC_TUBE_LANES=$l run f64_b${b}_l$l 300 python bench.py --dtype f64 --batch $b --steps 5 --warmup 8 --no-cpu --no-steady --no-extra
+      done; done ;;
     bench_quick) run bench_quick 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-steady ;;
     *) echo "unknown step $s" ;;
   esac

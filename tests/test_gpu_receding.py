@@ -300,43 +300,59 @@ def test_reference_call_pattern(dev):
     assert float(phi_xx[3, 3]) == 2.0 * stage_cost.__self__.cost.qb
 
 
-@pytest.mark.parametrize("m,gamma,alpha", [(1, 0.0, 0.0), (3, 0.3, 0.05), (8, 0.0, 0.0)])
-def test_receding_fused_instantiations_vs_generic(dev, m, gamma, alpha):
-    """The fused receding driver's other instantiations -- obstacle counts 1 / 3 / 8 (compile-time M) and the
-    general gain records (gamma != 0, alpha > 0: receding_fast_kernel<M, 0>) -- against the generic kernel on a
-    well-conditioned f64 workload (starts in the open, target beyond the obstacle field's first ring, H = 10):
-    exits identical and every recorded run within 1e-9 on >= 97 % of the runs (the two kernels' own roundings)."""
+@pytest.mark.parametrize("m,gamma,alpha", [(m, 0.0, 0.0) for m in range(1, 9)] + [(3, 0.3, 0.05), (8, 0.3, 0.05)])
+def test_receding_fused_instantiations_vs_generic(dev, oracle_lib, m, gamma, alpha):
+    """The fused receding driver's other instantiations -- every obstacle count 1-8 (compile-time M) and the
+    general gain records (gamma != 0, alpha > 0: receding_fast_kernel<M, 0>) -- against the generic kernel and
+    the oracle (plain build), f64, B = 256, H = 10, x0 ~ U[0,1]^2 x U[0, pi/2]; and the fused driver run
+    twice on the same inputs, bitwise equal.  This test found the M = 8 f64 defect of round 4 (run-to-run
+    different results with the obstacle table pinned in VGPRs).
+
+    The obstacles sit off the diagonal the runs move along (barrier active, no decision close to a tie): there
+    the three oracle builds agree on every run to 1e-14 (measured on the CPU; with obstacles on the paths, as
+    in the paper field's (4, 2) / (6, 6), the builds themselves agree on only 56-79 % of the runs at 1e-9 --
+    the chaotic regime of test_receding_fused_vs_generic).  Asserted: exits identical and every recorded run
+    within 1e-9 on >= 99 % of the runs, fused vs generic and both vs the oracle."""
     from diff_tube_mpc_strict_pt.core import nominal_receding
     from diff_tube_mpc_strict_pt.core.receding import receding_setup_from_config
     from _common import config
+    from oracle.oracle import Oracle
 
     cfg = json.loads(json.dumps(config()))
-    ring = [(4.0, 2.0), (2.0, 4.0), (4.0, 8.0), (8.0, 4.0), (6.0, 6.0), (9.0, 9.0), (1.0, 7.0), (7.0, 1.0)]
+    ring = [(8.0, 2.5), (2.5, 8.0), (9.5, 4.5), (4.5, 9.5), (6.5, 1.5), (1.5, 6.5), (9.0, 7.5), (7.5, 9.0)]
     cfg["environment"]["obstacles"] = [{"center": list(c), "radius": 0.8} for c in ring[:m]]
     cfg["dbas"]["gamma"], cfg["dbas"]["alpha"] = gamma, alpha
     problem, cost, icfg = receding_setup_from_config(cfg)
     assert len(problem.obstacles) == m
-    B, H = 256, 10
+    B, H, N = 256, 10, problem.horizon
     rng = np.random.default_rng(11)
     x0 = np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1)
     runs = []
-    for fast in ("1", "0"):
+    for fast in ("1", "1", "0"):
         monkey = pytest.MonkeyPatch()
         monkey.setenv("DTMPC_FAST", fast)
         r = nominal_receding(problem=problem, cost=cost, cfg=icfg, x0=torch.as_tensor(x0, device=dev), H=H, check=False)
         torch.cuda.synchronize()
         monkey.undo()
-        runs.append(r)
-    a, b = runs
-    ex = [np.stack([r.h_ran.cpu().numpy(), r.success_t.cpu().numpy(), r.collided.cpu().numpy(),
-                    r.status.cpu().numpy()], 1) for r in runs]
-    same = (ex[0] == ex[1]).all(1)
-    la = torch.cat([a.x, a.u, a.b[..., None]], -1).cpu().numpy()
-    lb = torch.cat([b.x, b.u, b.b[..., None]], -1).cpu().numpy()
-    mask = np.arange(H)[None, :] < a.h_ran.cpu().numpy()[:, None]
-    d = np.where(mask[..., None], np.abs(la - lb), 0).reshape(B, -1).max(1)
-    sc = np.where(mask[..., None], np.abs(lb), 0).reshape(B, -1).max(1) + 1.0
-    frac = float((d[same] / sc[same] <= 1e-9).mean())
-    print(f"[receding fused vs generic M={m} gamma={gamma} alpha={alpha}] exits equal {same.mean():.4f}, "
-          f"runs within 1e-9 {frac:.4f}, failures {int((a.status != 0).sum())} / {int((b.status != 0).sum())}")
-    assert same.mean() >= 0.97 and frac >= 0.97, (same.mean(), frac)
+        runs.append((torch.cat([r.x, r.u, r.b[..., None]], -1).cpu().numpy(), r.h_ran.cpu().numpy(),
+                     r.success_t.cpu().numpy(), r.collided.cpu().numpy().astype(np.int32), r.status.cpu().numpy()))
+    for k in range(5):  # the fused driver twice: bitwise
+        assert np.array_equal(runs[0][k], runs[1][k], equal_nan=True), k
+    del runs[1]
+    U = np.zeros((B, N, 2))
+    U[:, :, 0] = problem.u_max[0]
+    runs.append(Oracle(np.float64, nthreads=8).nominal_receding(problem.to_c(), cost.to_c(), icfg.to_c(), x0.copy(),
+                                                                H, 0.25, U)[:5])
+
+    def pair(a, b):
+        ex = (a[1] == b[1]) & (a[2] == b[2]) & (a[3] == b[3]) & (a[4] == b[4])
+        mask = np.arange(H)[None, :] < a[1][:, None]
+        d = np.where(mask[..., None], np.abs(a[0] - b[0]), 0).reshape(B, -1).max(1)
+        sc = np.where(mask[..., None], np.abs(b[0]), 0).reshape(B, -1).max(1) + 1.0
+        return float(ex.mean()), float((d[ex] / sc[ex] <= 1e-9).mean())
+
+    res = {"fused-generic": pair(runs[0], runs[1]), "fused-oracle": pair(runs[0], runs[2]),
+           "generic-oracle": pair(runs[1], runs[2])}
+    print(f"[receding instantiation M={m} gamma={gamma} alpha={alpha}] (exits equal, runs within 1e-9): {res}")
+    for k, (e, f) in res.items():
+        assert e == 1.0 and f >= 0.99, (k, res)
