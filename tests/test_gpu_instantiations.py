@@ -153,3 +153,43 @@ def test_general_step_instantiations(dev, tag, m, monkeypatch):
         lambda dt: GeneralTubeMPC(st, batch=B, device=dev, dtype=dt, disturbance="philox", seed=9),
         x0)
     _compare(f"general {tag} M={m}", runs, B, tol, need, truth)
+
+
+@pytest.mark.parametrize("m", [1, 3, 6, 8])
+def test_ilqr_instantiations_f64(dev, oracle_lib, m, monkeypatch):
+    """The standalone batched iLQR (ilqr_fast_kernel, four lanes at this batch) per obstacle count, f64, 10
+    iterations at tol 1e-3 from a constant warm start: fused vs the oracle held to the oracle builds' own
+    pairwise agreement (the tol exit makes a few trajectories decide at the cost's resolution), the generic
+    kernel likewise, and the fused solve twice bitwise equal."""
+    from diff_tube_mpc_strict_pt.core import ilqr_solve
+    from diff_tube_mpc_strict_pt.core.problem import ILQRConfig, paper_setup_from_config
+
+    from _common import oracles
+
+    st = paper_setup_from_config(_cfg(m))
+    B, N = 512, st.problem.horizon
+    x = _starts(B, torch.float64, dev).cpu().numpy()
+    x0 = np.concatenate([x, np.ones((B, 1))], 1)
+    V0 = np.zeros((B, N, 2))
+    V0[:, :, 0] = 10.0
+    ic = ILQRConfig(horizon=N, max_iter=10, tol=1e-3, line_search_alphas=st.ilqr_nom.line_search_alphas)
+    outs = []
+    for fast in ("1", "1", "0"):
+        monkeypatch.setenv("DTMPC_FAST", fast)
+        r = ilqr_solve(problem=st.problem, cost=st.nominal_cost, cfg=ic, x0=torch.as_tensor(x0, device=dev),
+                       V_init=torch.as_tensor(V0, device=dev), check=False)
+        torch.cuda.synchronize()
+        outs.append(r.V.reshape(B, -1).cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    del outs[1]
+    outs += [o.ilqr_solve(st.problem.to_c(), st.nominal_cost.to_c(), ic.to_c(), x0, V0)[1].reshape(B, -1)
+             for o in oracles(np.float64)]
+
+    def frac(a, b):
+        return float((np.abs(a - b).max(1) / (np.abs(b).max(1) + 1) <= 1e-8).mean())
+
+    builds = [frac(outs[i], outs[j]) for i in range(2, 5) for j in range(i + 1, 5)]
+    fo, go, fg = frac(outs[0], outs[2]), frac(outs[1], outs[2]), frac(outs[0], outs[1])
+    print(f"[ilqr f64 M={m}] within 1e-8: fused-oracle {fo:.4f} generic-oracle {go:.4f} fused-generic {fg:.4f}; "
+          f"oracle builds pairwise {[round(b, 4) for b in builds]}")
+    assert fo >= min(builds) - 0.03 and go >= min(builds) - 0.03, (fo, go, builds)
