@@ -88,13 +88,23 @@ def _truth(make, x0):
     return _snap(mpc)
 
 
-@pytest.mark.parametrize("m", range(1, 9))
+@pytest.mark.parametrize("m,g0", [(m, "") for m in range(1, 9)] + [(4, "0"), (5, "0"), (8, "0")])
 @pytest.mark.parametrize("tag", ["f64", "f32"])
-def test_tube_step_instantiations(dev, tag, m, monkeypatch):
+def test_tube_step_instantiations(dev, tag, m, g0, monkeypatch, request):
+    """g0 "0" (DTMPC_FAST_G0=0): the general gain records and recursion (tube_fast_kernel<M, P, 0>; the paper
+    mode's gamma is 0, so only this A/B switch reaches them), the f64 instantiations with the most scratch spill
+    traffic (up to 208 B per lane, hipcc -S).  Open defect: in f64 at M = 4 and 8 these
+    return non-finite statuses on some trajectories (M = 5 is correct) -- expected to fail, not reachable from a
+    product configuration (the switch is the only way in)."""
+    if tag == "f64" and g0 == "0" and m != 5:
+        request.node.add_marker(pytest.mark.xfail(reason="f64 general-record tube kernel at M != 5 (open defect)",
+                                                  strict=False))
     from diff_tube_mpc_strict_pt.core import TubeMPC
     from diff_tube_mpc_strict_pt.core.problem import paper_setup_from_config
 
     tdt, tol, need = BAND[tag]
+    if g0:
+        monkeypatch.setenv("DTMPC_FAST_G0", g0)
     st = paper_setup_from_config(_cfg(m))
     assert len(st.problem.obstacles) == m
     B = 1024
@@ -116,9 +126,10 @@ def test_tube_step_instantiations(dev, tag, m, monkeypatch):
             for k in NAMES:
                 assert np.array_equal(first[k], runs[0][k], equal_nan=True), k
     monkeypatch.setenv("DTMPC_FAST", "1")
+    monkeypatch.delenv("DTMPC_FAST_G0", raising=False)  # truth: the f64 step on its default records
     truth = None if tag == "f64" else _truth(
         lambda dt: TubeMPC(st, batch=B, device=dev, dtype=dt, disturbance="philox", seed=5), x0)
-    _compare(f"tube {tag} M={m}", runs, B, tol, need, truth)
+    _compare(f"tube {tag} M={m} G0={g0 or 2}", runs, B, tol, need, truth)
 
 
 @pytest.mark.parametrize("m", [1, 3, 8])
