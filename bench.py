@@ -49,7 +49,9 @@ from diff_tube_mpc_strict_pt.core.problem import paper_config, paper_setup_from_
 # SURVEY.md §8d algorithmic HBM bytes per trajectory per closed-loop step (phase-split tape traffic):
 # 10 nominal iterations x 7,652 B + 20 ancillary iterations x 9,676 B + one IFT pass 4,284 B.
 ALGO_BYTES_PER_TRAJ_STEP = 10 * 7652 + 20 * 9676 + 4284  # = 274,324
+NOMINAL_ITER_BYTES = 7652  # one nominal iLQR iteration of one trajectory, f32; x 2 in f64
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+VALU_ISSUE_CYCLES = 4.5  # cycles one wave64 VALU instruction costs its wave at one wave per SIMD (profiles/r02/issue_cost.txt)
 ITERS_PER_STEP = 10 + 20 + 1
 
 
@@ -84,11 +86,9 @@ def lib_sha256() -> str:
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def pmc_traffic(batch: int, kernel: str = "tube"):
-    """Per-launch HBM bytes of the dominant kernel from a committed rocprofv3 --pmc summary
-    (profiles/rNN/pmc_*.json, written by scripts/pmc_summary.py) for the SAME library build (sha256) and
-    batch, or (None, reason).  FETCH_SIZE / WRITE_SIZE are calibrated there on a known-byte launch
-    (MI355X_MICROARCH.md §HBM: gfx950 under-reports wide coalesced reads)."""
+def pmc_summary(batch: int, kernel: str = "tube"):
+    """The newest committed rocprofv3 --pmc summary (profiles/rNN/pmc_*.json, scripts/pmc_summary.py) of this
+    workload and batch for the SAME library build (sha256), or (None, reason)."""
     def newest_first(path):  # profiles/rNN/pmc_vMM.json: the highest round, then the highest version
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.relpath(path, REPO))]
 
@@ -101,13 +101,46 @@ def pmc_traffic(batch: int, kernel: str = "tube"):
             continue
         if int(d.get("batch", -1)) != batch or d.get("workload", "tube") != kernel:
             continue
-        if "tube_step_bytes_per_launch" not in d:
-            continue
         if d.get("lib_sha256") != want:
             best, why = None, f"newest PMC summary for this batch ({os.path.relpath(p, REPO)}) is of another library build"
             continue
-        best, why = float(d["tube_step_bytes_per_launch"]), os.path.relpath(p, REPO)
+        best, why = d, os.path.relpath(p, REPO)
     return best, why
+
+
+def issue_of(summary) -> dict | None:
+    """The instruction-issue roofline of the kernel from its PMC summary: VALU instructions per wave x 4.5 cycles
+    (what one wave64 VALU instruction costs its wave at one wave per SIMD, scripts/ubench/issue_cost.hip) over the
+    kernel's shader cycles (GRBM_GUI_ACTIVE / 8 XCDs, MI355X_MICROARCH.md: effective clock), and the SQ's own VALU
+    busy share of the wave cycles."""
+    if not summary:
+        return None
+    c = summary.get("counters_per_dispatch", {})
+    if not all(k in c for k in ("SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE")):
+        return None
+    per_wave = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+    cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+    out = {"valu_instr_per_wave": per_wave, "kernel_cycles": cycles,
+           "valu_issue_frac": per_wave * VALU_ISSUE_CYCLES / cycles,
+           "salu_instr_per_wave": c.get("SQ_INSTS_SALU", 0.0) / c["SQ_WAVES"]}
+    if "SQ_ACTIVE_INST_VALU" in c and "SQ_WAVE_CYCLES" in c:
+        out["valu_active_frac"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
+    ks = summary.get("kernel_trace") or {}
+    if ks.get("avg_ns"):
+        out["clock_ghz"] = cycles / ks["avg_ns"]
+    return out
+
+
+def pmc_traffic(batch: int, kernel: str = "tube"):
+    """Per-launch HBM bytes of the dominant kernel from a committed rocprofv3 --pmc summary
+    (profiles/rNN/pmc_*.json, written by scripts/pmc_summary.py) for the SAME library build (sha256) and
+    batch, or (None, reason).  FETCH_SIZE / WRITE_SIZE are calibrated there on a known-byte launch
+    (MI355X_MICROARCH.md §HBM: gfx950 under-reports wide coalesced reads)."""
+    d, why = pmc_summary(batch, kernel)
+    if d is None:
+        return None, why
+    b = d.get("kernel_bytes_per_launch", d.get("tube_step_bytes_per_launch"))
+    return (float(b), why) if b is not None else (None, why + " has no HBM counters")
 
 
 def cpu_baseline(setup, seconds_target: float = 15.0):
@@ -177,13 +210,15 @@ def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup
     iters = torch.zeros(B, dtype=torch.int32, device=dev)
     status = torch.zeros(B, dtype=torch.int32, device=dev)
     code = 0 if dt == torch.float32 else 1
-    lanes = int(lib.dtmpc_tube_lanes(B))
+    lanes = int(lib.dtmpc_tube_lanes_dtype(B, code))
     wb = int(lib.dtmpc_ilqr_workspace_bytes(code, N, B, lanes))
     work = torch.empty(max(wb, 1), dtype=torch.uint8, device=dev)
     fused = bool(lib.dtmpc_ilqr_fused_eligible(code, C.byref(spec), C.byref(cc), C.byref(ic)))  # the path that runs
 
-    def solve():
+    def solve(e0=None, e1=None):
         Us.copy_(U0)
+        if e0 is not None:
+            e0.record()
         if generic:
             _lib.check(lib.dtmpc_ilqr_solve(code, C.byref(spec), C.byref(cc), C.byref(ic), B, x0.data_ptr(), None,
                                             None, Xs.data_ptr(), Us.data_ptr(), Ks.data_ptr(), ks.data_ptr(),
@@ -194,25 +229,34 @@ def nominal_ddp_leg(dev, dtype_name: str, B: int = 4096, steps: int = 20, warmup
                                                None, Xs.data_ptr(), Us.data_ptr(), Ks.data_ptr(), ks.data_ptr(),
                                                iters.data_ptr(), status.data_ptr(), None, None, lanes, work.data_ptr(), wb,
                                                _lib.stream_of(x0)), "dtmpc_ilqr_solve_ws")
+        if e1 is not None:
+            e1.record()
 
     for _ in range(warmup):
         solve()
     torch.cuda.synchronize(dev)
+    # HIP events on the launch stream around the solve alone (the warm-start re-seed copy is outside them)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
     for e0, e1 in ev:
-        e0.record()
-        solve()
-        e1.record()
+        solve(e0, e1)
     torch.cuda.synchronize(dev)
     wall = (time.perf_counter() - t0) / steps
-    return {"workload": f"BASELINE config 2: batched nominal DDP, {cfg.max_iter} fixed iterations (tol=-1), "
-                        f"{len(cfg.line_search_alphas)} alphas, T={N}, zero warm start",
-            "batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall,
-            "kernel": ("generic ilqr_kernel" if generic or not fused else f"fused ilqr_fast_kernel, {lanes} lanes"),
-            "event_ms_median": float(np.median([a.elapsed_time(b) for a, b in ev])),
-            "value": B * cfg.max_iter / wall, "unit": "DDP iters/s",
-            "nonzero_status": int((status != 0).sum())}
+    kern = [a.elapsed_time(b) for a, b in ev]
+    out = {"workload": f"BASELINE config 2: batched nominal DDP, {cfg.max_iter} fixed iterations (tol=-1), "
+                       f"{len(cfg.line_search_alphas)} alphas, T={N}, zero warm start",
+           "batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall,
+           "kernel": ("generic ilqr_kernel" if generic or not fused else f"fused ilqr_fast_kernel, {lanes} lanes"),
+           "event_ms_median": float(np.median(kern)), "kernel_ms": float(np.mean(kern)),
+           "value": B * cfg.max_iter / wall, "unit": "DDP iters/s",
+           "nonzero_status": int((status != 0).sum())}
+    if not generic and fused:
+        # 7,652 algorithmic bytes per nominal iteration and trajectory (f32; f64 twice)
+        algo = NOMINAL_ITER_BYTES * cfg.max_iter * B * (2 if dtype_name == "f64" else 1)
+        wl = f"nominal_ddp_{dtype_name}"
+        traffic, src = pmc_traffic(B, kernel=wl)
+        out["roofline"] = roofline_of(algo, out["kernel_ms"], traffic, src, workload=wl, batch=B)
+    return out
 
 
 def warm_up(step, warmup: int, dev, min_launches: int = 8, max_launches: int = 40, rel: float = 0.01) -> int:
@@ -235,11 +279,20 @@ def warm_up(step, warmup: int, dev, min_launches: int = 8, max_launches: int = 4
         last = t
 
 
-def roofline_of(algo_bytes: float, kernel_ms: float, traffic=None, traffic_src=None) -> dict:
+def roofline_of(algo_bytes: float, kernel_ms: float, traffic=None, traffic_src=None, workload=None,
+                batch=None) -> dict:
+    """HBM roofline of one kernel: algorithmic bytes per launch over its mean HIP-event time, the calibrated
+    PMC bytes beside them, and (from the same PMC summary) the instruction-issue roofline (issue_of)."""
     achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-            "algo_bytes_per_launch": algo_bytes}
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+           "algo_bytes_per_launch": algo_bytes}
+    if workload is not None:
+        summ, _ = pmc_summary(batch, workload)
+        out["issue"] = issue_of(summ)
+        if out["issue"] is not None:
+            out["issue"]["source"] = traffic_src
+    return out
 
 
 def tube_leg(dev, dtype_name: str, B: int, steps: int, warmup: int, adapt: bool = True, workload: str = ""):
@@ -266,11 +319,12 @@ def tube_leg(dev, dtype_name: str, B: int, steps: int, warmup: int, adapt: bool 
     wall = (time.perf_counter() - t0) / steps
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in kev]))
     algo = ALGO_BYTES_PER_TRAJ_STEP * B * (2 if dtype_name == "f64" else 1)
-    traffic, src = pmc_traffic(B, kernel="tube" if dtype_name == "f32" else "tube_f64")
+    wl = "tube" if dtype_name == "f32" else "tube_f64"
+    traffic, src = pmc_traffic(B, kernel=wl)
     out = {"batch": B, "dtype": dtype_name, "ms_per_step": 1e3 * wall, "warmup_run": nwarm,
            "kernel_ms": kern_ms, "adapt": adapt,
            "value": B * ITERS_PER_STEP / wall, "unit": "DDP+IFT iters/s",
-           "roofline": roofline_of(algo, kern_ms, traffic, src),
+           "roofline": roofline_of(algo, kern_ms, traffic, src, workload=wl, batch=B),
            "flagged_trajectories": int((mpc.status != 0).sum()), "lanes": mpc.lanes,
            # the fused kernel in this precision (f64: csrc/dtmpc_fast64.hip) unless switched off for A/B
            "kernel": ("generic tube_step_kernel"
@@ -308,10 +362,18 @@ def receding_leg(dev, dtype_name: str, B: int = 65536, H: int = 20, reps: int = 
         ms.append(e0.elapsed_time(e1))
     t = float(np.median(ms))
     solves = int(r.h_ran.sum())
+    iters = int(r.iters.sum())
+    # algorithmic bytes: SURVEY.md §8d's 7,652 B per nominal iLQR iteration (f32; f64 twice) times the iterations
+    # the runs actually took (each run's own tol exits and run exits: dtmpc_nominal_receding_it)
+    algo = NOMINAL_ITER_BYTES * iters * (2 if dtype_name == "f64" else 1)
+    wl = f"receding_{dtype_name}"
+    traffic, src = pmc_traffic(B, kernel=wl)
     return {"workload": "receding-horizon nominal MPC (run_nominal.py), B runs x H steps, tol=1e-3, 7 alphas",
             "batch": B, "H": H, "dtype": dtype_name, "ms_per_receding_step": t / H, "launch_ms": t,
-            "ilqr_solves_per_s": solves / (t * 1e-3), "solves": solves, "failed": int((r.status != 0).sum()),
-            "success": int((r.success_t >= 0).sum()), "collided": int(r.collided.sum())}
+            "ilqr_solves_per_s": solves / (t * 1e-3), "solves": solves, "ilqr_iterations": iters,
+            "failed": int((r.status != 0).sum()),
+            "success": int((r.success_t >= 0).sum()), "collided": int(r.collided.sum()),
+            "roofline": roofline_of(algo, t, traffic, src, workload=wl, batch=B)}
 
 
 def _free_port() -> int:
@@ -350,8 +412,9 @@ def main() -> None:
     ap.add_argument("--no-steady", action="store_true", help="skip the free-running (warm-started) loop field")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary legs (f64 tube step, config-2 nominal DDP at B = 4096)")
-    ap.add_argument("--workload", default="tube", choices=["tube", "nominal-ddp"],
-                    help="nominal-ddp: print only the BASELINE config-2 line (one GPU)")
+    ap.add_argument("--workload", default="tube", choices=["tube", "nominal-ddp", "receding"],
+                    help="nominal-ddp: print only the BASELINE config-2 line (one GPU); receding: only the receding "
+                         "driver's leg (one GPU; profiling runs)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -383,6 +446,14 @@ def main() -> None:
                           "ms_per_step": leg["ms_per_step"], "higher_is_better": True, "scaling": "strong",
                           "vs_baseline": None, "dtype": args.dtype, "data": "synthetic x0 (bench.initial_states)",
                           "config": {"workload": leg["workload"], "global_batch": leg["batch"]}, "leg": leg}))
+        return
+    if args.workload == "receding":
+        if world != 1 or args.dry_run:
+            raise SystemExit("--workload receding is a one-GPU leg")
+        leg = receding_leg(dev, args.dtype, B=args.batch)
+        print(json.dumps({"metric": "receding-horizon iLQR solves/sec, Dubins+DBaS T=50", "value": leg["ilqr_solves_per_s"],
+                          "unit": "iLQR solves/s", "n_gpus": 1, "ms_per_step": leg["ms_per_receding_step"],
+                          "higher_is_better": True, "dtype": args.dtype, "leg": leg}))
         return
     dtype = torch.float32 if args.dtype == "f32" else torch.float64
     setup = bench_setup(args.dtype)
@@ -513,7 +584,9 @@ def main() -> None:
         "flagged_trajectories": int(cnt[0]),
         "event_ms_per_step_median": float(np.median(step_ms)),
         "warmup_run": nwarm,
-        "roofline": roofline_of(algo_bytes, kern_ms, traffic, traffic_src),
+        "roofline": roofline_of(algo_bytes, kern_ms, traffic, traffic_src,
+                                workload=None if args.dry_run else ("tube" if args.dtype == "f32" else "tube_f64"),
+                                batch=hi - lo),
     }
     out["steady_state"] = steady
     if world == 1 and not args.dry_run and not args.no_extra:

@@ -85,12 +85,63 @@ constexpr int kTight = 16;
 // kWrap: the nominal target cost with the heading error wrapped to (-pi, pi] (run_nominal.py:297-324, the
 // receding-horizon driver's stage / terminal cost and derivatives); only the receding kernel sets it.
 constexpr int kWrap = 32;
+// kLds (f64): the obstacle table read from the workgroup's LDS copy at each use (obs_lds) instead of being held
+// in registers -- the f64 instantiations whose table cannot be pinned in VGPRs without spilling (tab_flag below)
+constexpr int kLds = 64;
 template <int M>
 struct Obs {
   static constexpr int n = M & (kTight - 1);
   static constexpr bool tight = (M & kTight) != 0;
   static constexpr bool wrap = (M & kWrap) != 0;
+  static constexpr bool lds = (M & kLds) != 0;
 };
+
+#if DTMPC_FAST_F64
+// the f64 kernels' obstacle table in LDS (x, y, r^2, -) per obstacle, written once per workgroup (obs_fill)
+__shared__ real obs_lds[32];
+#endif
+// obstacle i of the table: the registers of FP, or (kLds) the LDS copy, read through a volatile pointer so that
+// every use loads it again -- a hoisted load would hold the table in VGPRs for the whole loop, which is what kLds
+// instantiations cannot afford
+template <int M>
+__device__ __forceinline__ real ocx(const FP& p, int i) {
+#if DTMPC_FAST_F64
+  if (Obs<M>::lds) return ((volatile __attribute__((address_space(3))) real*)obs_lds)[4 * i];
+#endif
+  return p.cx[i];
+}
+template <int M>
+__device__ __forceinline__ real ocy(const FP& p, int i) {
+#if DTMPC_FAST_F64
+  if (Obs<M>::lds) return ((volatile __attribute__((address_space(3))) real*)obs_lds)[4 * i + 1];
+#endif
+  return p.cy[i];
+}
+template <int M>
+__device__ __forceinline__ real or2(const FP& p, int i) {
+#if DTMPC_FAST_F64
+  if (Obs<M>::lds) return ((volatile __attribute__((address_space(3))) real*)obs_lds)[4 * i + 2];
+#endif
+  return p.r2[i];
+}
+// kLds kernels: the table into LDS from the kernarg copy, before any lane returns (one barrier)
+template <int M>
+__device__ __forceinline__ void obs_fill(const FP& p) {
+#if DTMPC_FAST_F64
+  if (Obs<M>::lds) {
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        obs_lds[4 * j] = p.cx[j];
+        obs_lds[4 * j + 1] = p.cy[j];
+        obs_lds[4 * j + 2] = p.r2[j];
+        obs_lds[4 * j + 3] = 0.0;
+      }
+    }
+    __syncthreads();
+  }
+#endif
+}
 
 struct FCost {  // nominal: target; ancillary: tracking (terminal weight = stage weight)
   real Q0, Q1, Q2, R0, R1, Qf0, Qf1, Qf2, qb;
@@ -119,6 +170,8 @@ struct FArgs {
   real* work;  // workspace: the per-lane records below, one buffer resource (< 2^31 bytes)
   unsigned wsz;  // bytes of it the records use
   unsigned oXn, oUn, oXa, oUa, oK, ok, oA8, oA2;  // byte offsets of the record arrays in the workspace
+  unsigned oPH;  // the split step's hand-over [3][Bc] int: nominal tape's record offsets, status | iterations << 8
+  int phase;     // dtmpc_tube_state.phase: 0 whole step, 1 nominal solve, 2 the rest
   const real* theta;
   real* partials;
   real* log;
@@ -408,15 +461,46 @@ constexpr double kDC1 = 4.16666666666666019037e-02, kDC2 = -1.388888888887410957
 #ifndef DTMPC_FAST64_FAR
 #define DTMPC_FAST64_FAR 1
 #endif
+#ifndef DTMPC_FAST64_FARRET
+#define DTMPC_FAST64_FARRET 1
+#endif
+struct SinCos {
+  double s, c;
+};
+#if DTMPC_FAST64_FARRET
+// returned by value (v0..v3): no out-parameter, so no local of the caller ever has its address taken
 #if DTMPC_FAST64_FAR == 1
-__device__ __attribute__((noinline)) void sincos_far(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __attribute__((noinline)) SinCos sincos_far(double x) {
+#else
+__device__ __forceinline__ SinCos sincos_far(double x) {
+#endif
+  SinCos r;
+  sincos(x, &r.s, &r.c);
+  return r;
+}
+#elif DTMPC_FAST64_FAR == 1
+__device__ __attribute__((noinline)) void sincos_far(double x, double* s, double* c) {
+#ifdef DTMPC_FAST_DIAG_FARPRINT
+  printf("DIAG far x=%.17g\n", x);
+#endif
+  sincos(x, s, c);
+#ifdef DTMPC_FAST_DIAG_FARWAIT
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
+}
 #else
 __device__ __forceinline__ void sincos_far(double x, double* s, double* c) { sincos(x, s, c); }
 #endif
 __device__ __forceinline__ void vsincos(real x, real& sn, real& cs) {
 #if DTMPC_FAST64_FAR != 2
   if (__builtin_expect(!(__builtin_fabs(x) <= 1048576.0), 0)) {
+#if DTMPC_FAST64_FARRET
+    const SinCos r = sincos_far(x);
+    sn = r.s;
+    cs = r.c;
+#else
     sincos_far(x, &sn, &cs);
+#endif
     return;
   }
 #endif
@@ -547,9 +631,9 @@ __device__ __forceinline__ V h_sm(const FP& p, V px, V py) {
   V hi[MO], hm;
 #pragma unroll
   for (int i = 0; i < MO; ++i) {
-    const V dx = px - p.cx[i];
-    const V dy = py - p.cy[i];
-    hi[i] = ffma(dx, dx, dy * dy) - p.r2[i];
+    const V dx = px - ocx<M>(p, i);
+    const V dy = py - ocy<M>(p, i);
+    hi[i] = ffma(dx, dx, dy * dy) - or2<M>(p, i);
     hm = i == 0 ? hi[0] : vmin(hm, hi[i]);
   }
   const V zmax = p.neg_beta * hm;
@@ -566,14 +650,23 @@ template <int M>
 __device__ __forceinline__ real h_grad(const FP& p, real px, real py, real& gx, real& gy) {
 #pragma clang fp contract(off)
   constexpr int MO = Obs<M>::n;
-  real z[MO], hh[MO], zmax = 0.f;
+  // kLds (f64): the per-obstacle values are evaluated again in the sum pass instead of kept (bitwise the same)
+  constexpr bool TWO = Obs<M>::lds;
+  constexpr int MK = TWO ? 1 : MO;
+  real z[MK], hh[MK], dxs[MK], dys[MK], zmax = 0.f;
 #pragma unroll
   for (int i = 0; i < MO; ++i) {
-    const real dx = px - p.cx[i];
-    const real dy = py - p.cy[i];
-    hh[i] = dx * dx + dy * dy - p.r2[i];
-    z[i] = p.neg_beta * hh[i];
-    zmax = (i == 0 || z[i] > zmax) ? z[i] : zmax;
+    const real dx = px - ocx<M>(p, i);
+    const real dy = py - ocy<M>(p, i);
+    const real h = dx * dx + dy * dy - or2<M>(p, i);
+    const real zi = p.neg_beta * h;
+    if (!TWO) {
+      dxs[i] = dx;
+      dys[i] = dy;
+      hh[i] = h;
+      z[i] = zi;
+    }
+    zmax = (i == 0 || zi > zmax) ? zi : zmax;
   }
 #if !DTMPC_FAST_F64
   const real zl = zmax * real(1.44269504088896341);
@@ -581,17 +674,28 @@ __device__ __forceinline__ real h_grad(const FP& p, real px, real py, real& gx, 
   real se = 0.f, sx = 0.f, sy = 0.f;
 #pragma unroll
   for (int i = 0; i < MO; ++i) {
+    real dx, dy, zi;
+    if (TWO) {
+      dx = px - ocx<M>(p, i);
+      dy = py - ocy<M>(p, i);
+      zi = p.neg_beta * (dx * dx + dy * dy - or2<M>(p, i));
+    } else {
+      dx = dxs[i];
+      dy = dys[i];
+      zi = z[i];
+    }
 #if DTMPC_FAST_F64
     // the generic kernel's h_grad (dtmpc_device.hpp), with the smooth-min's rule for negligible terms (smterm)
-    const real x = z[i] - zmax;
+    const real x = zi - zmax;
     real e = 0.0;
     if (__builtin_amdgcn_ballot_w64(smneed(x))) e = smexp(x);
 #else
-    const real e = __builtin_amdgcn_exp2f(__builtin_fmaf(hh[i], p.nbl2e, -zl));
+    (void)zi;
+    const real e = __builtin_amdgcn_exp2f(__builtin_fmaf(hh[TWO ? 0 : i], p.nbl2e, -zl));
 #endif
     se += e;
-    sx += e * (2.f * (px - p.cx[i]));
-    sy += e * (2.f * (py - p.cy[i]));
+    sx += e * (2.f * dx);  // = 2 (px - cx_i), the first loop's difference
+    sy += e * (2.f * dy);
   }
   const real inv = m_rcp(se);
   gx = sx * inv;
@@ -720,9 +824,14 @@ __device__ __forceinline__ V kdot(const f4& K, V e0, V e1, V e2, V e3) {
 
 // ---------------------------------------------------------------------------------------------
 // the tapes one iLQR solve works on
-template <bool TRACK, bool G0, bool RG0, int P, int NCV = NC>
+// RROLL (TRACK): the references are an exact rollout of their controls from X_ref[0] by this kernel's own
+// arithmetic -- the tube step's and the general path's ancillary solves, whose references are the nominal solve's
+// tape -- so the f32 line search may re-roll them instead of reading them (LS_RECOMP).  The standalone iLQR takes
+// any caller references (X_ref need not be a rollout of U_ref): RROLL = false, every reference row is read.
+template <bool TRACK, bool G0, bool RG0, int P, int NCV = NC, bool RROLL = true>
 struct Solve {
   static_assert(NCV == NC || (NCV == 4 && P != 4), "four lanes split six candidates");
+  static constexpr bool rroll = RROLL;
   static constexpr bool g0 = G0;    // gamma = 0: the compact gain records (Gains)
   static constexpr bool ric0 = RG0; // gamma = 0: the Riccati step without the barrier state's zero column
   static constexpr int lanes = P;   // lanes per trajectory
@@ -1377,18 +1486,29 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
     C.a1[q] = ffma(dv, sn[q], C.a1[q]);
     C.a2[q] = ffma(f2(p.dt), u1[q], C.a2[q]);
   }
-  // smooth-min h over the M obstacles (h_sm), all pairs together
+  // smooth-min h over the M obstacles (h_sm), all pairs together.  TWO (kLds, f64): the h_i are not kept between
+  // the min and the exp pass but evaluated again (the same operations, so bitwise the same values) -- at M = 8
+  // the kept 8 x NPR pairs of doubles were what made the general-record kernels spill (build.py check_resources)
   constexpr int MO = Obs<M>::n;
-  f2 hi[MO][NPR], hm[NPR];
+  constexpr bool TWO = Obs<M>::lds;
+  f2 hi[TWO ? 1 : MO][NPR], hm[NPR];
+  auto hval = [&](int i, int q) {
+    const f2 dx = C.a0[q] - ocx<M>(p, i);
+    const f2 dy = C.a1[q] - ocy<M>(p, i);
+    return ffma(dx, dx, dy * dy) - or2<M>(p, i);
+  };
 #pragma unroll
-  for (int i = 0; i < MO; ++i)
+  for (int i = 0; i < MO; ++i) {
+    const real cxi = ocx<M>(p, i), cyi = ocy<M>(p, i), r2i = or2<M>(p, i);  // one read per obstacle (kLds)
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
-      const f2 dx = C.a0[q] - p.cx[i];
-      const f2 dy = C.a1[q] - p.cy[i];
-      hi[i][q] = ffma(dx, dx, dy * dy) - p.r2[i];
-      hm[q] = i == 0 ? hi[0][q] : vmin(hm[q], hi[i][q]);
+      const f2 dx = C.a0[q] - cxi;
+      const f2 dy = C.a1[q] - cyi;
+      const f2 h = ffma(dx, dx, dy * dy) - r2i;
+      if (!TWO) hi[i][q] = h;
+      hm[q] = i == 0 ? h : vmin(hm[q], h);
     }
+  }
   f2 zmax[NPR], zl[NPR], se[NPR], z[NPR];
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
@@ -1403,7 +1523,7 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
     bool need = false;
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
-      x[q] = smarg(p, hi[i][q], zmax[q]);
+      x[q] = smarg(p, TWO ? hval(i, q) : hi[TWO ? 0 : i][q], zmax[q]);
       need = need || smneed(x[q]);
       e[q] = f2(0.0);
     }
@@ -1415,7 +1535,7 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
 #else
 #pragma unroll
     for (int q = 0; q < NPR; ++q) {
-      const f2 e = smterm(p, hi[i][q], zmax[q], zl[q]);
+      const f2 e = smterm(p, hi[TWO ? 0 : i][q], zmax[q], zl[q]);
       se[q] = i == 0 ? e : se[q] + e;  // = 0 + e_0 + ...: e_0 >= 0, so 0 + e_0 == e_0 bitwise
     }
 #endif
@@ -1544,9 +1664,10 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   // the same Dubins arithmetic that produced them (init_tape / commit / the nominal's solve: rollout(x0, U)),
   // so they are bit for bit the stored rows; their b is never needed (K's b column is zero at gamma = 0)
   constexpr bool RC = DTMPC_FAST_LS_RECOMP && SV::g0 && !DTMPC_FAST_F64;
+  constexpr bool RCR = RC && SV::rroll;  // the references re-rolled too (only when they are a device rollout)
   auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
   real o0 = x0[0], o1 = x0[1], o2 = x0[2], q0 = 0.f, q1 = 0.f, q2 = 0.f;
-  if (RC && TRACK) {
+  if (RCR && TRACK) {
     const f4 R0 = S.xr(0);
     q0 = R0.x;
     q1 = R0.y;
@@ -1558,7 +1679,7 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
       L.X1 = o1;
       L.X2 = o2;
       dubins(p, o0, o1, o2, L.V0, L.V1);
-      if (TRACK) {
+      if (TRACK && RCR) {
         L.r0 = q0;
         L.r1 = q1;
         L.r2 = q2;
@@ -1567,25 +1688,25 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
     }
   };
   StepIn A, Bs, Cs, Ds;
-  load_step<TRACK, !RC, SV, !RC>(A, S, 0);
-  load_step<TRACK, !RC, SV, !RC>(Bs, S, ix(1));
+  load_step<TRACK, !RC, SV, !RCR>(A, S, 0);
+  load_step<TRACK, !RC, SV, !RCR>(Bs, S, ix(1));
   for (int k = 0; k < N; k += 4) {
-    load_step<TRACK, !RC, SV, !RC>(Cs, S, ix(k + 2));
+    load_step<TRACK, !RC, SV, !RCR>(Cs, S, ix(k + 2));
     roll(A);
     ls_step<TRACK, M, NPR, SV::g0>(p, c, A, C, u0, u1);
     keep(k, u0, u1);
     if (k + 1 >= N) break;
-    load_step<TRACK, !RC, SV, !RC>(Ds, S, ix(k + 3));
+    load_step<TRACK, !RC, SV, !RCR>(Ds, S, ix(k + 3));
     roll(Bs);
     ls_step<TRACK, M, NPR, SV::g0>(p, c, Bs, C, u0, u1);
     keep(k + 1, u0, u1);
     if (k + 2 >= N) break;
-    load_step<TRACK, !RC, SV, !RC>(A, S, ix(k + 4));
+    load_step<TRACK, !RC, SV, !RCR>(A, S, ix(k + 4));
     roll(Cs);
     ls_step<TRACK, M, NPR, SV::g0>(p, c, Cs, C, u0, u1);
     keep(k + 2, u0, u1);
     if (k + 3 >= N) break;
-    load_step<TRACK, !RC, SV, !RC>(Bs, S, ix(k + 5));
+    load_step<TRACK, !RC, SV, !RCR>(Bs, S, ix(k + 5));
     roll(Ds);
     ls_step<TRACK, M, NPR, SV::g0>(p, c, Ds, C, u0, u1);
     keep(k + 3, u0, u1);
@@ -1815,6 +1936,36 @@ __device__ __forceinline__ void ls_stat(int trk, int best, real al, const FIlqr&
 }
 #endif
 
+#ifdef DTMPC_FAST_DIAG
+// diagnostics builds (scripts/diag_f64.sh, not the product): every kernel's kernarg segment starts with its FP, so
+// the problem constants the solver holds in registers (the pinned obstacle table, the scalars) can be compared
+// with the segment's copy at every phase boundary; the first lanes that disagree, or whose solve goes
+// non-finite, print where.  The general path forms its DBaS constants on the device, so only the table and the
+// dynamics constants are compared there.
+__device__ __forceinline__ void diag_p(const FP& p, int where, int it) {
+  const FP* q = (const FP*)__builtin_amdgcn_kernarg_segment_ptr();
+  int bad = -1;
+  real v = 0, w = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (__builtin_bit_cast(unsigned long long, (double)p.cx[j]) != __builtin_bit_cast(unsigned long long, (double)q->cx[j])) { bad = j; v = p.cx[j]; w = q->cx[j]; }
+    if (__builtin_bit_cast(unsigned long long, (double)p.cy[j]) != __builtin_bit_cast(unsigned long long, (double)q->cy[j])) { bad = 10 + j; v = p.cy[j]; w = q->cy[j]; }
+    if (__builtin_bit_cast(unsigned long long, (double)p.r2[j]) != __builtin_bit_cast(unsigned long long, (double)q->r2[j])) { bad = 20 + j; v = p.r2[j]; w = q->r2[j]; }
+  }
+  if (p.dt != q->dt) { bad = 30; v = p.dt; w = q->dt; }
+  if (p.umax0 != q->umax0 || p.umin0 != q->umin0 || p.umax1 != q->umax1 || p.umin1 != q->umin1) { bad = 31; v = p.umax0; w = q->umax0; }
+  if (p.neg_beta != q->neg_beta || p.neg_inv_beta != q->neg_inv_beta) { bad = 32; v = p.neg_beta; w = q->neg_beta; }
+  if (p.eps != q->eps) { bad = 33; v = p.eps; w = q->eps; }
+  if (p.N != q->N) { bad = 34; v = p.N; w = q->N; }
+  if (bad >= 0)
+    printf("DIAG const blk=%d thr=%d where=%d it=%d field=%d have=%.17g want=%.17g\n", (int)blockIdx.x,
+           (int)threadIdx.x, where, it, bad, (double)v, (double)w);
+}
+#define DIAG_P(p, where, it) diag_p(p, where, it)
+#else
+#define DIAG_P(p, where, it) ((void)0)
+#endif
+
 // P = 4 tape slots: slot q of the solve's X / U records at lane offset base + q * stride
 struct SlotMap {
   unsigned bx, sx, bu, su;  // X: base (trajectory * 16), slot stride (Bc * 16); U: (trajectory * 8), (Bc * 8)
@@ -1854,12 +2005,19 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
   int st = 0;
   int cur = kSlotInit;  // P = 4: the current tape's slot
   pf.mark(ph);
+  DIAG_P(p, TRACK ? 100 : 0, -1);
   for (int it = 0; it < cf.max_iter; ++it) {
     iters = it + 1;
     if (!backward<TRACK, M>(p, c, cf.reg, S, h)) {
       st = DTMPC_ST_NONFINITE;
+#ifdef DTMPC_FAST_DIAG
+      printf("DIAG backward non-finite blk=%d thr=%d h=%d trk=%d it=%d x0=(%.17g %.17g %.17g %.17g)\n", (int)blockIdx.x,
+             (int)threadIdx.x, h, (int)TRACK, it, (double)x0[0], (double)x0[1], (double)x0[2], (double)x0[3]);
+      DIAG_P(p, TRACK ? 101 : 1, it);
+#endif
       break;
     }
+    DIAG_P(p, TRACK ? 102 : 2, it);
     pf.mark(ph + 1);
     real bestJ, al;
     int bc;
@@ -1880,8 +2038,15 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
 #endif
     if (best < 0) {
       st = DTMPC_ST_NONFINITE;
+#ifdef DTMPC_FAST_DIAG
+      printf("DIAG line search non-finite blk=%d thr=%d h=%d trk=%d it=%d Jprev=%.17g bestJ=%.17g x0=(%.17g %.17g %.17g %.17g)\n",
+             (int)blockIdx.x, (int)threadIdx.x, h, (int)TRACK, it, (double)Jcur, (double)bestJ, (double)x0[0],
+             (double)x0[1], (double)x0[2], (double)x0[3]);
+      DIAG_P(p, TRACK ? 103 : 3, it);
+#endif
       break;
     }
+    DIAG_P(p, TRACK ? 104 : 4, it);
     if (ch && h == 0) ch[it * chs] = (signed char)best;
     if (al != 0.f) {
       if (P == 4) {
@@ -2100,6 +2265,9 @@ __device__ __forceinline__ const char* kargs_ws() { return (const char*)kargs()-
 #ifndef DTMPC_FAST_PIN
 #define DTMPC_FAST_PIN 1
 #endif
+#ifndef DTMPC_FAST_PIN64_MAX
+#define DTMPC_FAST_PIN64_MAX 5
+#endif
 // the problem constants of one phase; the obstacle table pinned in VGPRs (every candidate of every
 // step reads it; in scalar registers it is what the compiler would spill first).  f64 pins at most five
 // obstacles (30 VGPRs; the paper's M = 5): the f64 receding kernel at M = 8 with its 48-VGPR table spilled
@@ -2109,7 +2277,7 @@ __device__ __forceinline__ const char* kargs_ws() { return (const char*)kargs()-
 template <int M>
 __device__ __forceinline__ FP pin_p(FP p) {
 #if DTMPC_FAST_PIN
-  if (DTMPC_FAST_F64 && Obs<M>::n > 5) return p;
+  if (Obs<M>::lds || (DTMPC_FAST_F64 && Obs<M>::n > DTMPC_FAST_PIN64_MAX)) return p;
 #pragma unroll
   for (int j = 0; j < Obs<M>::n; ++j) {
     real vx = p.cx[j], vy = p.cy[j], vr = p.r2[j];
@@ -2128,12 +2296,30 @@ __device__ __forceinline__ FP phase_p() {
   return pin_p<M>(kargs()->p);
 }
 
+// Where an f64 instantiation keeps its obstacle table (round 5).  Every f64 fused kernel must run without a
+// private segment (build.py check_resources: the f64 defects of rounds 3-4 all came from f64 kernels that kept
+// values in scratch inside per-lane divergent loops).  The table pinned in VGPRs (pin_p) fits
+// beside the compact gamma = 0 records up to DTMPC_FAST_PIN64_MAX obstacles; the general records (GM = 0, and the
+// general path's solves, which hold both record forms) and larger tables read it from LDS at each use (kLds).
+// DTMPC_FAST64_TAB: 1 that rule (default), 2 LDS in every f64 kernel, 0 never LDS (the round-4 forms, A/B).
+#ifndef DTMPC_FAST64_TAB
+#define DTMPC_FAST64_TAB 1
+#endif
+template <int M, int GM>
+constexpr int tab_flag() {
+  return (DTMPC_FAST_F64 && (DTMPC_FAST64_TAB == 2 ||
+                             (DTMPC_FAST64_TAB == 1 && (GM == 0 || Obs<M>::n > DTMPC_FAST_PIN64_MAX))))
+             ? kLds
+             : 0;
+}
+
 // GM: 0 general, 1 gamma = 0 gain records, 2 gamma = 0 gain records + Riccati step (the default at gamma = 0)
 // One wave per SIMD at every lane count (amdgpu_waves_per_eu(1, 1)): the whole 512-register budget.
 template <int M, int P, int GM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 tube_fast_kernel(FK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
+  constexpr int ML = M | tab_flag<M, GM>();  // M with the table placement (kLds: LDS, f64 only)
   (void)kk;  // read through kargs()
   __shared__ f4 lds[kBlock / 64 * DTMPC_TUBE_SUMS / 4];  // the workgroup sums at the end
   const int B = kargs()->a.B, Bc = kargs()->a.Bc, i0 = kargs()->a.i0;
@@ -2149,6 +2335,7 @@ tube_fast_kernel(FK kk) {
     const int n = kargs()->a.stagger * (int)(blockIdx.x & 7) / 8;
     for (int r = 0; r < n; ++r) __builtin_amdgcn_s_sleep(127);
   }
+  obs_fill<ML>(kargs()->p);
   Prof pf;
   pf.start();
   if (t < Bc) {
@@ -2175,8 +2362,20 @@ tube_fast_kernel(FK kk) {
       y2 = K->a.xbar[2 * nb + i];
       yb = K->a.bbar[i];
     }
+    const int phase = kargs()->a.phase;  // uniform: which part of the step this launch runs
+    // the split step's hand-over (phase 1 -> 2): the nominal tape's final record offsets (P = 4: its slot) and
+    // the nominal solve's status and iterations, [3][Bc] ints after the records
+    int* const hand = (int*)((char*)kargs()->a.work + kargs()->a.oPH) + t;
     Solve<false, G0, RG0, P> Sn;
-    {  // nominal MPC (fixed weights, :813-857)
+    if (phase == 2) {  // the nominal was solved by this step's phase-1 launch
+      KArg* K = kargs();
+      Sn.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
+      Sn.XA = RA{K->a.oXn, NS * cb * (16u * ES), (unsigned)hand[0]};
+      Sn.UA = RA{K->a.oUn, NS * cb * (8u * ES), (unsigned)hand[Bc]};
+      const int w2 = hand[2 * Bc];
+      st = w2 & 0xff;
+      itn = w2 >> 8;
+    } else {  // nominal MPC (fixed weights, :813-857)
       KArg* K = kargs();
       Sn.r = __builtin_amdgcn_make_buffer_rsrc(K->a.work, 0, (int)K->a.wsz, 0x00020000);
       Sn.XA = RA{K->a.oXn, NS * cb * (16u * ES), x0lo};
@@ -2188,13 +2387,20 @@ tube_fast_kernel(FK kk) {
       Sn.G.k = RA{K->a.ok, cb * (8u * ES), l8};
       Sn.X = Soa<4>{(char*)K->a.Xnom, 4u * bb, L};
       Sn.U = Soa<2>{(char*)K->a.Unom, 2u * bb, L};
-      const FP p = phase_p<M>();
+      const FP p = phase_p<ML>();
       const FCost cn = K->cn;
       const FIlqr cfn = K->cfn;
       const real xn0[4] = {y0, y1, y2, yb};
       const DecRec dr{K->a.choices ? K->a.choices + i : nullptr, K->a.costs ? K->a.costs + i : nullptr, nb};
-      st |= ilqr<false, M, P>(p, cn, cfn, xn0, Sn, h, sm, itn, pf, dr);
+      st |= ilqr<false, ML, P>(p, cn, cfn, xn0, Sn, h, sm, itn, pf, dr);
     }
+    if (phase == 1) {  // hand over to the phase-2 launch; the plant state and theta are untouched
+      if (h == 0) {
+        hand[0] = (int)Sn.XA.lo;
+        hand[Bc] = (int)Sn.UA.lo;
+        hand[2 * Bc] = st | (itn << 8);
+      }
+    } else {
     FCost ca;  // ancillary weights theta (shared by the batch), terminal weight Qa (:885, :891)
     {
       const real* th = kargs()->a.theta;
@@ -2219,25 +2425,26 @@ tube_fast_kernel(FK kk) {
       Sa.G.k = RA{K->a.ok, cb * (8u * ES), l8};
       Sa.X = Soa<4>{(char*)K->a.Xaux, 4u * bb, L};
       Sa.U = Soa<2>{(char*)K->a.Uaux, 2u * bb, L};
-      const FP p = phase_p<M>();
+      const FP p = phase_p<ML>();
       const FIlqr cfa = K->cfa;
       const real xa0[4] = {x0, x1, x2, xb};
       const size_t o = (size_t)K->cfn.max_iter * nb + i;
       const DecRec dr{K->a.choices ? K->a.choices + o : nullptr, K->a.costs ? K->a.costs + 8 * (o - i) + i : nullptr, nb};
-      st |= ilqr<true, M, P>(p, ca, cfa, xa0, Sa, h, sm, ita, pf, dr);
+      st |= ilqr<true, ML, P>(p, ca, cfa, xa0, Sa, h, sm, ita, pf, dr);
     }
     pf.mark(8);
     {  // upper loss, DOC sensitivity and gradient (:915-976)
       KArg* K = kargs();
       const RA A8{K->a.oA8, cb * (32u * ES), l32}, A2{K->a.oA2, cb * (8u * ES), l8};
-      const FP p = phase_p<M>();
-      st |= sensitivity<M>(p, ca, Sa, A8, A2, acc);
+      const FP p = phase_p<ML>();
+      st |= sensitivity<ML>(p, ca, Sa, A8, A2, acc);
+      DIAG_P(p, 200, st);
     }
     pf.mark(9);
     {  // plant step with disturbance, nominal propagation (:990-1001), log, warm-start shift
       KArg* K = kargs();
       const FArgs& a = K->a;
-      const FP p = phase_p<M>();
+      const FP p = phase_p<ML>();
       // the plans' first controls, from the records (the ABI tapes already hold the shifted warm starts)
       const f2 ua = rld2(Sa.r, Sa.UA, 0, 0), un = rld2(Sa.r, Sn.UA, 0, 0);
       const real u0 = ua.x, u1 = ua.y;
@@ -2273,22 +2480,26 @@ tube_fast_kernel(FK kk) {
         for (int j = 0; j < 7; ++j) lg[(11 + j) * nb + i] = acc[j];
       }
       {
-        real q0 = x0, q1 = x1, q2 = x2, qb = xb, Bc = barrier_at<M>(p, x0, x1);
-        fhat<M>(p, q0, q1, q2, qb, u0, u1, Bc);
+        real q0 = x0, q1 = x1, q2 = x2, qb = xb, Bc = barrier_at<ML>(p, x0, x1);
+        fhat<ML>(p, q0, q1, q2, qb, u0, u1, Bc);
         a.x[i] = q0 + w[0];
         a.x[nb + i] = q1 + w[1];
         a.x[2 * nb + i] = q2 + w[2];
         a.b[i] = qb;
       }
       {
-        real q0 = y0, q1 = y1, q2 = y2, qb = yb, Bc = barrier_at<M>(p, y0, y1);
-        fhat<M>(p, q0, q1, q2, qb, v0, v1, Bc);
+        real q0 = y0, q1 = y1, q2 = y2, qb = yb, Bc = barrier_at<ML>(p, y0, y1);
+        fhat<ML>(p, q0, q1, q2, qb, v0, v1, Bc);
         a.xbar[i] = q0;
         a.xbar[nb + i] = q1;
         a.xbar[2 * nb + i] = q2;
         a.bbar[i] = qb;
       }
       acc[7] = 1.f;
+      DIAG_P(p, 300, st);
+#ifdef DTMPC_FAST_DIAG
+      if (st && h == 0) printf("DIAG status traj=%d st=%d itn=%d ita=%d\n", i, st, itn, ita);
+#endif
       // healthy trajectories only (status 0 and every gradient component within the bound, NaN failing
       // the test); a trajectory's lanes count once
       real gm = m_abs(acc[1]);
@@ -2307,8 +2518,10 @@ tube_fast_kernel(FK kk) {
       }
     }
     pf.mark(10);
+    }  // phase != 1
   }
   pf.flush();
+  if (kargs()->a.phase == 1) return;  // the step's sums come from its phase-2 launch (uniform)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   real ws[DTMPC_TUBE_SUMS];
 #pragma unroll
@@ -2391,6 +2604,8 @@ ilqr_fast_kernel(IK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
   (void)kk;  // read through ikargs()
   const IArgs& a = ikargs()->a;
+  constexpr int ML = M | tab_flag<M, GM>();
+  obs_fill<ML>(ikargs()->p);
   const int B = a.B, Bc = a.Bc, i0 = a.i0;
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
   const int t = gl / P, h = gl % P;
@@ -2403,7 +2618,7 @@ ilqr_fast_kernel(IK kk) {
   const unsigned cb = (unsigned)Bc, l8 = (unsigned)t * (8u * ES), l16 = (unsigned)t * (16u * ES), l32 = (unsigned)t * (32u * ES);
   const SlotMap sm{l16, cb * (16u * ES), l8, cb * (8u * ES)};
   const unsigned x0lo = P == 4 ? l16 + kSlotInit * cb * (16u * ES) : l16, u0lo = P == 4 ? l8 + kSlotInit * cb * (8u * ES) : l8;
-  Solve<TRACK, G0, RG0, P> S;
+  Solve<TRACK, G0, RG0, P, NC, false> S;  // caller references: read, never re-rolled (RROLL)
   S.r = __builtin_amdgcn_make_buffer_rsrc(a.work, 0, (int)a.wsz, 0x00020000);
   S.XA = RA{a.oX, NS * cb * (16u * ES), x0lo};
   S.UA = RA{a.oU, NS * cb * (8u * ES), u0lo};
@@ -2413,7 +2628,7 @@ ilqr_fast_kernel(IK kk) {
   S.G.k = RA{a.ok, cb * (8u * ES), l8};
   S.X = Soa<4>{(char*)a.X, 4u * bb, L};
   S.U = Soa<2>{(char*)a.U, 2u * bb, L};
-  const FP p = pin_p<M>(ikargs()->p);
+  const FP p = pin_p<ML>(ikargs()->p);
   const int N = p.N;
   if (TRACK) {  // the references into records (the lanes of a trajectory split the rows; one wave: in order)
     for (int k = h; k <= N; k += P) {
@@ -2432,7 +2647,7 @@ ilqr_fast_kernel(IK kk) {
   int it = 0;
   Prof pf;
   pf.start();
-  const int st = ilqr<TRACK, M, P, false>(p, c, cf, x0, S, h, sm, it, pf, dr);
+  const int st = ilqr<TRACK, ML, P, false>(p, c, cf, x0, S, h, sm, it, pf, dr);
   // the last backward pass's gains out to the ABI arrays (G0 records: K's barrier column is exactly 0);
   // max_iter = 0: no backward pass ran and the records were never written -- zeros, as the generic kernel
   // leaves the zeroed arrays
@@ -2480,6 +2695,7 @@ struct RArgs {
   int* success_t;
   int* collided;
   int* status;
+  int* iters;  // [B] the run's total iLQR iterations (the receding leg's algorithmic bytes), or NULL
   real* work;
   unsigned wsz, oX, oU, oK, ok;
 };
@@ -2503,8 +2719,8 @@ __device__ __forceinline__ real h_true_min(const FP& p, real px, real py) {
   real m = 0.f;
 #pragma unroll
   for (int i = 0; i < Obs<M>::n; ++i) {
-    const real dx = px - p.cx[i], dy = py - p.cy[i];
-    const real hi = dx * dx + dy * dy - p.r2[i];
+    const real dx = px - ocx<M>(p, i), dy = py - ocy<M>(p, i);
+    const real hi = dx * dx + dy * dy - or2<M>(p, i);
     m = i == 0 ? hi : m_min(m, hi);
   }
   return m;
@@ -2514,8 +2730,10 @@ template <int M, int GM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 receding_fast_kernel(RK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
-  constexpr int MW = M | kWrap;
+  constexpr int ML = M | tab_flag<M, GM>();
+  constexpr int MW = ML | kWrap;
   (void)kk;  // read through rkargs()
+  obs_fill<ML>(rkargs()->p);
   const RArgs& a = rkargs()->a;
   const int B = a.B, Bc = a.Bc, i0 = a.i0;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2536,17 +2754,18 @@ receding_fast_kernel(RK kk) {
   S.G.k = RA{a.ok, cb * (8u * ES), l8};
   S.X = Soa<4>{(char*)a.Xs, 4u * bb, L};
   S.U = Soa<2>{(char*)a.U, 2u * bb, L};
-  const FP p = pin_p<M>(rkargs()->p);
+  const FP p = pin_p<ML>(rkargs()->p);
   const FCost c = rkargs()->c;
   const FIlqr cf = rkargs()->cf;
   const int N = p.N, H = a.H;
   real x[4] = {a.x0[i], a.x0[nb + i], a.x0[2 * nb + i], 0.f};
-  x[3] = barrier_at<M>(p, x[0], x[1]);  // dbas_init_b0 (run_nominal.py:279)
-  int st = 0, ran = H, sidx = -1, coll = 0;
+  x[3] = barrier_at<ML>(p, x[0], x[1]);  // dbas_init_b0 (run_nominal.py:279)
+  int st = 0, ran = H, sidx = -1, coll = 0, itot = 0;
   for (int ts = 0; ts < H; ++ts) {
     int it = 0;
     Prof pf;
     st |= ilqr<false, MW, 1, false>(p, c, cf, x, S, 0, sm, it, pf, DecRec{nullptr, nullptr, 0});
+    itot += it;
     const f2 u = rld2(S.r, S.UA, 0, 0);  // the plan's first control (the records hold the solved plan)
     real* lg = a.log + (size_t)ts * 6 * nb + i;
     lg[0] = x[0];
@@ -2559,7 +2778,7 @@ receding_fast_kernel(RK kk) {
       ran = ts + 1;
       break;
     }
-    if (h_true_min<M>(p, x[0], x[1]) <= real(0)) {  // collision (run_nominal.py:388-397)
+    if (h_true_min<ML>(p, x[0], x[1]) <= real(0)) {  // collision (run_nominal.py:388-397)
       coll = 1;
       ran = ts + 1;
       break;
@@ -2574,8 +2793,8 @@ receding_fast_kernel(RK kk) {
       }
     }
     // x <- f_hat(x, u0) (run_nominal.py:377-378)
-    real Bc = barrier_at<M>(p, x[0], x[1]);
-    fhat<M, G0>(p, x[0], x[1], x[2], x[3], u.x, u.y, Bc);
+    real Bc = barrier_at<ML>(p, x[0], x[1]);
+    fhat<ML, G0>(p, x[0], x[1], x[2], x[3], u.x, u.y, Bc);
     // U <- [U[1:], U[-1]] (run_nominal.py:405-406) on the ABI warm start the next solve starts from
     for (int k = 0; k + 1 < N; ++k) {
       S.U.st(k, 0, S.U.ld(k + 1, 0));
@@ -2586,6 +2805,7 @@ receding_fast_kernel(RK kk) {
   a.success_t[i] = sidx;
   a.collided[i] = coll;
   a.status[i] |= st;
+  if (a.iters) a.iters[i] = itot;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2665,6 +2885,8 @@ template <int M, int P, int NCV>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 general_solve_fast_kernel(GSK kk) {
   (void)kk;  // read through gskargs()
+  constexpr int ML = M | tab_flag<M, 0>();  // both record forms in one kernel: placed as the general records
+  obs_fill<ML>(gskargs()->p);
   const GSArgs& a = gskargs()->a;
   const int B = a.B, Bc = a.Bc, i0 = a.i0;
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2688,21 +2910,21 @@ general_solve_fast_kernel(GSK kk) {
   RA XN{a.oXn, NS * cb * (16u * ES), x0lo}, UN{a.oUn, NS * cb * (8u * ES), u0lo};
   {  // nominal MPC with theta-bar (:217-291)
     const GPar<real> pn = gpar_from<real>(a.theta + DTMPC_P_COUNT, true);
-    const FP p = pin_p<M | kTight>(general_fp(gskargs()->p, pn));
+    const FP p = pin_p<ML | kTight>(general_fp(gskargs()->p, pn));
     const FCost cn{pn.Q[0], pn.Q[1], pn.Q[2], pn.R[0], pn.R[1], pn.Qf[0], pn.Qf[1], pn.Qf[2], pn.qb, a.tgt};
     const FIlqr cfn = gskargs()->cfn;
     const real xn0[4] = {a.xbar[i], a.xbar[nb + i], a.xbar[2 * nb + i], a.bbar[i]};
     const Soa<4> X{(char*)a.Xnom, 4u * bb, L};
     const Soa<2> U{(char*)a.Unom, 2u * bb, L};
     if (pn.gamma == 0.f)
-      st |= general_solve<false, M | kTight, P, NCV, true>(p, cn, cfn, xn0, r, XN, UN, XN, UN, G, X, U, h, sm, itn, pf);
+      st |= general_solve<false, ML | kTight, P, NCV, true>(p, cn, cfn, xn0, r, XN, UN, XN, UN, G, X, U, h, sm, itn, pf);
     else
-      st |= general_solve<false, M | kTight, P, NCV, false>(p, cn, cfn, xn0, r, XN, UN, XN, UN, G, X, U, h, sm, itn, pf);
+      st |= general_solve<false, ML | kTight, P, NCV, false>(p, cn, cfn, xn0, r, XN, UN, XN, UN, G, X, U, h, sm, itn, pf);
   }
   {  // ancillary MPC with theta tracking the nominal plan as solved (:296-392)
     RA XA{a.oXa, NS * cb * (16u * ES), x0lo}, UA{a.oUa, NS * cb * (8u * ES), u0lo};
     const GPar<real> pa = gpar_from<real>(a.theta, false);
-    const FP p = pin_p<M>(general_fp(gskargs()->p, pa));
+    const FP p = pin_p<ML>(general_fp(gskargs()->p, pa));
     const FCost ca{pa.Q[0], pa.Q[1], pa.Q[2], pa.R[0], pa.R[1], pa.Qf[0], pa.Qf[1], pa.Qf[2], pa.qb,
                    f4{0.f, 0.f, 0.f, 0.f}};
     const FIlqr cfa = gskargs()->cfa;
@@ -2710,9 +2932,9 @@ general_solve_fast_kernel(GSK kk) {
     const Soa<4> X{(char*)a.Xaux, 4u * bb, L};
     const Soa<2> U{(char*)a.Uaux, 2u * bb, L};
     if (pa.gamma == 0.f)
-      st |= general_solve<true, M, P, NCV, true>(p, ca, cfa, xa0, r, XA, UA, XN, UN, G, X, U, h, sm, ita, pf);
+      st |= general_solve<true, ML, P, NCV, true>(p, ca, cfa, xa0, r, XA, UA, XN, UN, G, X, U, h, sm, ita, pf);
     else
-      st |= general_solve<true, M, P, NCV, false>(p, ca, cfa, xa0, r, XA, UA, XN, UN, G, X, U, h, sm, ita, pf);
+      st |= general_solve<true, ML, P, NCV, false>(p, ca, cfa, xa0, r, XA, UA, XN, UN, G, X, U, h, sm, ita, pf);
   }
   if (h == 0) {
     a.sst[i] = st;
@@ -2790,11 +3012,11 @@ static void fast_p(const dtmpc_spec* sp, FK_NS::FP& p) {
 // sensitivity scratch A8 [N][Bc][8], A2 [N][Bc][2].  All of it addressed through one buffer resource, so a
 // chunk's records stay below 2^31 bytes (tube_fast_chunk_max); larger batches run in chunks.
 struct FastLayout {
-  unsigned oXn, oXa, oUn, oUa, oK, ok, oA8, oA2, wsz;
+  unsigned oXn, oXa, oUn, oUa, oK, ok, oA8, oA2, oPH, wsz;
 };
 static int64_t fast_bytes_per_traj(int N, int lanes) {
   const int64_t ns = lanes == 4 ? FK_NS::kSlots : 1;
-  return ns * ((int64_t)(N + 1) * 32 * ES + (int64_t)N * 16 * ES) + (int64_t)N * 80 * ES;
+  return ns * ((int64_t)(N + 1) * 32 * ES + (int64_t)N * 16 * ES) + (int64_t)N * 80 * ES + 12;  // + hand-over
 }
 static FastLayout fast_layout(int N, int64_t Bc, int lanes) {
   const int64_t ns = lanes == 4 ? FK_NS::kSlots : 1;
@@ -2809,7 +3031,8 @@ static FastLayout fast_layout(int N, int64_t Bc, int lanes) {
   f.ok = f.oK + K;
   f.oA8 = f.ok + k;
   f.oA2 = f.oA8 + K;
-  f.wsz = f.oA2 + k;
+  f.oPH = f.oA2 + k;
+  f.wsz = f.oPH + (unsigned)(Bc * 12);
   return f;
 }
 int64_t FKN(tube_fast_chunk_max)(int N, int lanes) {
@@ -2871,6 +3094,7 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
     a.whi[f] = real(cf->w_high[f]);
   }
   const int lanes = S->lanes;
+  a.phase = S->phase;
   // gamma = 0 (the paper's DBaS): the compact gain records (FK_NS::Gains) and the Riccati step without the
   // barrier state's zero column (riccati_pk<true>).  DTMPC_FAST_G0 (environment, read at each call) = 0
   // keeps the general records and recursion, = 1 the compact records with the general recursion: the
@@ -2887,6 +3111,8 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
   // from the state (dtmpc_tube_chunk, validated against the workspace by dtmpc_tube_step)
   // (f64 records are twice as large: its chunk is at most half the f32 one, dtmpc_tube_workspace_bytes)
   const int64_t cmax = FKN(tube_fast_chunk_max)(N, lanes), chunk = S->chunk < cmax ? S->chunk : cmax;
+  // a split step keeps the nominal solve's records between its two launches: one chunk's worth of workspace
+  if (S->phase != 0 && B > chunk) return set_err(DTMPC_ERR_BAD_ARG, "a split step (state->phase 1 / 2) needs B <= chunk");
   for (int64_t c0 = 0; c0 < B; c0 += chunk) {
     const int64_t Bc = B - c0 < chunk ? B - c0 : chunk;
     a.i0 = (int)c0;
@@ -2900,6 +3126,7 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
     a.ok = f.ok;
     a.oA8 = f.oA8;
     a.oA2 = f.oA2;
+    a.oPH = f.oPH;
     a.wsz = f.wsz;
     const int bs = tube_block(B, lanes);  // 64 while the batch leaves SIMDs idle: one wave per workgroup
     const dim3 grid = dim3((unsigned)((Bc * lanes + bs - 1) / bs));
@@ -3034,12 +3261,13 @@ int FKN(launch_ilqr_fast)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmp
 }
 
 // the receding-horizon driver on the same solver (dtmpc_nominal_receding): the fast configuration with the
-// nominal target cost, wrapped or not, one lane per trajectory
+// nominal target cost and its heading error wrapped (run_nominal.py:297-324; receding_fast_kernel compiles the
+// wrapped cost in, M | kWrap), one lane per trajectory.  An unwrapped target cost runs the generic receding_kernel.
 bool FKN(receding_fast_eligible)(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf) {
   const char* e = getenv("DTMPC_FAST");
   if (e && e[0] == '0' && e[1] == 0) return false;
   if (DTMPC_FAST_F64 && (e = getenv("DTMPC_FAST64")) && e[0] == '0' && e[1] == 0) return false;
-  if (dtype != kFastDtype || !fast_spec_ok(sp) || c->kind != DTMPC_COST_TARGET) return false;
+  if (dtype != kFastDtype || !fast_spec_ok(sp) || c->kind != DTMPC_COST_TARGET || !c->wrap_angle) return false;
   return make_ilqr<real>(*cf).nc == FK_NS::NC;
 }
 static int64_t receding_fast_bytes_per_traj(int N) {  // records X, U, K, k + the ABI-layout plan
@@ -3049,7 +3277,7 @@ size_t FKN(receding_fast_workspace_bytes)(int N, int64_t B) { return (size_t)B *
 
 int FKN(launch_receding_fast)(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, int H,
                               double success_r, const void* x0, void* U, void* log, int* h_ran, int* success_t,
-                              int* collided, int* status, void* work, hipStream_t st) {
+                              int* collided, int* status, int* iters, void* work, hipStream_t st) {
   const int N = sp->horizon;
   FK_NS::RK kk;
   std::memset(&kk, 0, sizeof(kk));
@@ -3068,6 +3296,7 @@ int FKN(launch_receding_fast)(const dtmpc_spec* sp, const dtmpc_cost* cp, const 
   a.success_t = success_t;
   a.collided = collided;
   a.status = status;
+  a.iters = iters;
   // the ABI-layout plan after every chunk's records (the records of one chunk below 2^31 bytes)
   const int64_t rec = receding_fast_bytes_per_traj(N) - (int64_t)(N + 1) * 16 * ES;
   const int64_t chunk = ((int64_t)0x7fffffff / rec) / kBlock * kBlock;

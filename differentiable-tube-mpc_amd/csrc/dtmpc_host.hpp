@@ -207,12 +207,12 @@ bool receding_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c
 size_t receding_fast_workspace_bytes(int N, int64_t B);
 int launch_receding_fast(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, int H,
                          double success_r, const void* x0, void* U, void* log, int* h_ran, int* success_t,
-                         int* collided, int* status, void* work, hipStream_t st);
+                         int* collided, int* status, int* iters, void* work, hipStream_t st);
 bool receding_fast_eligible64(int dtype, const dtmpc_spec* sp, const dtmpc_cost* c, const dtmpc_ilqr_cfg* cf);
 size_t receding_fast_workspace_bytes64(int N, int64_t B);
 int launch_receding_fast64(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, int H,
                            double success_r, const void* x0, void* U, void* log, int* h_ran, int* success_t,
-                           int* collided, int* status, void* work, hipStream_t st);
+                           int* collided, int* status, int* iters, void* work, hipStream_t st);
 // the general path's two solves on the same solver (dtmpc_general_step); per-trajectory solve status to sst
 bool general_fast_eligible(int dtype, const dtmpc_spec* sp, const dtmpc_general_cfg* cf);
 int launch_general_solve_fast(const dtmpc_spec* sp, const dtmpc_general_cfg* cf, int64_t B,

@@ -259,10 +259,15 @@ int tube_block(int64_t B, int lanes) {
   return (DTMPC_TUBE_SMALL_BLOCK && B * lanes < lane_slots()) ? 64 : kBlock;
 }
 
-static int tube_lanes_default(int64_t B) {
+// f64 (round 5): the fused f64 step is instruction-bound at every batch (no packed f64 VALU), so four lanes --
+// the line search split four ways, the linearisation shared -- pay for their duplicated Riccati recursion up to
+// 4 B <= slots (B <= 16,384: 8.11 ms at four lanes vs 8.83 at two, profiles/r04/f64_lanes_v5.txt); above it one
+// lane (B = 65,536: 13.7 ms vs 19.1 at two, 37.5 at four).
+static int tube_lanes_default(int64_t B, int dtype = DTMPC_F32) {
   const char* e = getenv("DTMPC_TUBE_LANES");
   if (e && (e[0] == '1' || e[0] == '2' || e[0] == '4') && e[1] == 0) return e[0] - '0';
   const int64_t slots = lane_slots();
+  if (dtype == DTMPC_F64) return 4 * B <= slots ? 4 : 1;
   return 8 * B <= slots ? 4 : 2 * B <= slots ? 2 : 1;
 }
 
@@ -660,7 +665,7 @@ int dtmpc_ilqr_solve(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
 size_t dtmpc_ilqr_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t lanes) {
   if (dtype != DTMPC_F32 && dtype != DTMPC_F64) return 0;
   if (horizon < 1 || horizon > DTMPC_MAX_HORIZON || B < 1) return 0;
-  if (lanes == 0) lanes = tube_lanes_default(B);
+  if (lanes == 0) lanes = tube_lanes_default(B, dtype);
   if (lanes != 1 && lanes != 2 && lanes != 4) return 0;
   return dtype == DTMPC_F64 ? ilqr_fast_workspace_bytes64(horizon, B, lanes) : ilqr_fast_workspace_bytes(horizon, B, lanes);
 }
@@ -681,7 +686,7 @@ int dtmpc_ilqr_solve_ws(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cos
   if ((e = check_cost(cost, Xref, Uref))) return e;
   if ((e = check_ilqr(cfg))) return e;
   if (!x0 || !X || !U || !K || !kff || !status) return set_err(DTMPC_ERR_BAD_ARG, "NULL array");
-  if (lanes == 0) lanes = tube_lanes_default(B);
+  if (lanes == 0) lanes = tube_lanes_default(B, dtype);
   if (lanes != 1 && lanes != 2 && lanes != 4) return set_err(DTMPC_ERR_BAD_ARG, "lanes must be 0, 1, 2 or 4");
   if (ilqr_fast_eligible(dtype, spec, cost, cfg))
     return launch_ilqr_fast(spec, cost, cfg, B, x0, Xref, Uref, X, U, K, kff, iters, status, (signed char*)choices,
@@ -770,6 +775,10 @@ size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t
 }
 
 int32_t dtmpc_tube_lanes(int64_t B) { return tube_lanes_default(B); }
+int32_t dtmpc_tube_lanes_dtype(int64_t B, int dtype) {
+  if (dtype != DTMPC_F32 && dtype != DTMPC_F64) return 0;
+  return tube_lanes_default(B, dtype);
+}
 
 int64_t dtmpc_tube_partials_count(int64_t B, int32_t lanes) {
   if (B < 1 || (lanes != 1 && lanes != 2 && lanes != 4)) return 0;
@@ -807,12 +816,20 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
   }
   if (cfg->disturbance == 0 && !w) return set_err(DTMPC_ERR_BAD_ARG, "injected disturbance w is NULL");
   if (cfg->disturbance != 0 && cfg->disturbance != 1) return set_err(DTMPC_ERR_BAD_ARG, "bad disturbance mode");
+  if (S->phase < 0 || S->phase > 2) return set_err(DTMPC_ERR_BAD_ARG, "state->phase must be 0, 1 or 2");
+  if (S->phase != 0 && !dtmpc_tube_split_supported(dtype, spec, cfg))
+    return set_err(DTMPC_ERR_BAD_ARG, "a split step (state->phase 1 / 2) needs the fused kernel");
   hipStream_t st = (hipStream_t)stream;
   if (tube_fast_eligible(dtype, spec, cfg)) return launch_tube_fast(spec, cfg, B, global_offset, step, S, w, st);
   if (tube_fast_eligible64(dtype, spec, cfg)) return launch_tube_fast64(spec, cfg, B, global_offset, step, S, w, st);
   if (dtype == DTMPC_F32) return launch_tube<float>(spec, cfg, B, global_offset, step, S, w, st);
   if (dtype == DTMPC_F64) return launch_tube<double>(spec, cfg, B, global_offset, step, S, w, st);
   return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+}
+
+int32_t dtmpc_tube_split_supported(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg) {
+  if (!spec || !cfg) return 0;
+  return (tube_fast_eligible(dtype, spec, cfg) || tube_fast_eligible64(dtype, spec, cfg)) ? 1 : 0;
 }
 
 int dtmpc_partials_reduce(int dtype, int64_t n, const void* partials, void* sums, void* stream) {

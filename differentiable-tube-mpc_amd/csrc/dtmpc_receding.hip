@@ -26,6 +26,7 @@ struct RecedingArgs {
   int* success_t;
   int* collided;
   int* status;
+  int* iters;  // [B] total iLQR iterations of each run, or NULL
 };
 
 // true min_i h_i(x) over the circles (run_nominal.py:390-396)
@@ -49,11 +50,12 @@ __global__ void __launch_bounds__(kBlock) receding_kernel(DSpec<T> s, DCost<T> c
   const bool has_obs = s.agg != DTMPC_OBS_NONE && s.M > 0;
   T x[4] = {a.x0[i], a.x0[nb + i], a.x0[2 * nb + i], T(0)};
   x[3] = barrier_of_state(s, x[0], x[1]);  // dbas_init_b0 (:279)
-  int st = 0, ran = a.H, sidx = -1, coll = 0;
+  int st = 0, ran = a.H, sidx = -1, coll = 0, itot = 0;
   Prof pr;
   for (int t = 0; t < a.H; ++t) {
     int it = 0;
     st |= ilqr_traj<T, NA>(s, c, cfg, x, X, U, GainsSoA<T>{K, kf}, none, 0, none, it, pr, 0);
+    itot += it;
     T u0[1] = {U.at(0, 2, 0)}, u1[1] = {U.at(0, 2, 1)};
     lg.at(t, 6, 0) = x[0];
     lg.at(t, 6, 1) = x[1];
@@ -93,12 +95,13 @@ __global__ void __launch_bounds__(kBlock) receding_kernel(DSpec<T> s, DCost<T> c
   a.success_t[i] = sidx;
   a.collided[i] = coll;
   a.status[i] |= st;
+  if (a.iters) a.iters[i] = itot;
 }
 
 template <typename T>
 static int launch_receding(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtmpc_ilqr_cfg* cf, int64_t B, int H,
                            double success_r, const void* x0, void* U, void* log, int* h_ran, int* success_t,
-                           int* collided, int* status, void* work, hipStream_t st) {
+                           int* collided, int* status, int* iters, void* work, hipStream_t st) {
   DSpec<T> s = make_spec<T>(*sp);
   DCost<T> c = make_cost<T>(*cp);
   DIlqr<T> cfg = make_ilqr<T>(*cf);
@@ -119,6 +122,7 @@ static int launch_receding(const dtmpc_spec* sp, const dtmpc_cost* cp, const dtm
   a.success_t = success_t;
   a.collided = collided;
   a.status = status;
+  a.iters = iters;
   switch (cfg.nc) {
 #define CASE(n)                                                                                     \
   case n: hipLaunchKernelGGL((receding_kernel<T, n>), grid_for(B), dim3(kBlock), 0, st, s, c, cfg, a); break;
@@ -144,10 +148,10 @@ size_t dtmpc_receding_workspace_bytes(int dtype, int32_t horizon, int64_t B) {
   return generic > fused ? generic : fused;
 }
 
-int dtmpc_nominal_receding(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, const dtmpc_ilqr_cfg* cfg,
-                           int64_t B, int32_t H, double success_radius, const void* x0, void* U, void* log,
-                           int32_t* h_ran, int32_t* success_t, int32_t* collided, int32_t* status, void* work,
-                           void* stream) {
+int dtmpc_nominal_receding_it(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, const dtmpc_ilqr_cfg* cfg,
+                              int64_t B, int32_t H, double success_radius, const void* x0, void* U, void* log,
+                              int32_t* h_ran, int32_t* success_t, int32_t* collided, int32_t* status, int32_t* iters,
+                              void* work, void* stream) {
   int e = check_spec(spec, B);
   if (e) return e;
   if ((e = check_ilqr(cfg))) return e;
@@ -160,17 +164,25 @@ int dtmpc_nominal_receding(int dtype, const dtmpc_spec* spec, const dtmpc_cost* 
   // the paper configuration on the fused solver (DTMPC_FAST=0 / DTMPC_FAST64=0: the generic one below)
   if (receding_fast_eligible(dtype, spec, cost, cfg))
     return launch_receding_fast(spec, cost, cfg, B, H, success_radius, x0, U, log, h_ran, success_t, collided, status,
-                                work, st);
+                                iters, work, st);
   if (receding_fast_eligible64(dtype, spec, cost, cfg))
     return launch_receding_fast64(spec, cost, cfg, B, H, success_radius, x0, U, log, h_ran, success_t, collided,
-                                  status, work, st);
+                                  status, iters, work, st);
   if (dtype == DTMPC_F32)
     return launch_receding<float>(spec, cost, cfg, B, H, success_radius, x0, U, log, h_ran, success_t, collided, status,
-                                  work, st);
+                                  iters, work, st);
   if (dtype == DTMPC_F64)
     return launch_receding<double>(spec, cost, cfg, B, H, success_radius, x0, U, log, h_ran, success_t, collided,
-                                   status, work, st);
+                                   status, iters, work, st);
   return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
+}
+
+int dtmpc_nominal_receding(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost, const dtmpc_ilqr_cfg* cfg,
+                           int64_t B, int32_t H, double success_radius, const void* x0, void* U, void* log,
+                           int32_t* h_ran, int32_t* success_t, int32_t* collided, int32_t* status, void* work,
+                           void* stream) {
+  return dtmpc_nominal_receding_it(dtype, spec, cost, cfg, B, H, success_radius, x0, U, log, h_ran, success_t, collided,
+                                   status, nullptr, work, stream);
 }
 
 }  // extern "C"

@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_OBS = 16
 MAX_ALPHAS = 8
 MAX_HORIZON = 512
@@ -115,7 +115,7 @@ class DtmpcTubeState(C.Structure):
         ("status", C.c_void_p),
         ("iters", C.c_void_p),
         ("lanes", C.c_int32),
-        ("pad_", C.c_int32),
+        ("phase", C.c_int32),
         ("n_partials", C.c_int64),
         ("chunk", C.c_int64),
         ("work_bytes", C.c_int64),
@@ -206,6 +206,8 @@ PROTOTYPES = {
     "dtmpc_tube_chunk": (I64, [I32, I32]),
     "dtmpc_tube_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64, I32, I64]),
     "dtmpc_tube_lanes": (I32, [I64]),
+    "dtmpc_tube_lanes_dtype": (I32, [I64, C.c_int]),
+    "dtmpc_tube_split_supported": (I32, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcTubeCfg)]),
     "dtmpc_tube_partials_count": (I64, [I64, I32]),
     "dtmpc_tube_step": (
         C.c_int,
@@ -247,6 +249,9 @@ PROTOTYPES = {
     "dtmpc_nominal_receding": (
         C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, I32, C.c_double,
                   P, P, P, P, P, P, P, P, P]),
+    "dtmpc_nominal_receding_it": (
+        C.c_int, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcCost), C.POINTER(DtmpcIlqrCfg), I64, I32, C.c_double,
+                  P, P, P, P, P, P, P, P, P, P]),
 }
 
 

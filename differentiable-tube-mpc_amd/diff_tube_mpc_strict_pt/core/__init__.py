@@ -1,5 +1,7 @@
 """Core API: typed problem (problem), batched DDP/IFT entry points (ddp), closed loop (tube_mpc),
-control parameterisations (control) and tanh-box cost derivatives (cost_derivs)."""
+control parameterisations (control) and tanh-box cost derivatives (cost_derivs); the reference's autograd
+fallbacks (autodiff) and helpers (utils) under its own names (/root/reference core/__init__.py:22-31)."""
+from .autodiff import compute_jacobian, grad_hess_x, grad_hess_xu
 from .control import BoxClampControl, BoxTanhControl, tanh_box_eval
 from .cost_derivs import auxiliary_cost_derivs, nominal_cost_derivs
 from .ddp import (
@@ -29,9 +31,16 @@ from .problem import (
     tracking_cost,
 )
 from .receding import RecedingResult, nominal_receding, receding_setup_from_config
+from .utils import quadratic_cost_derivs_diagonal, regularize_matrix, solve_psd
 from .tube_mpc import ExperimentTrajectories, GeneralTubeMPC, TubeMPC, allreduce_sums, run_closed_loop_experiment, shard_range
 
 __all__ = [
+    "compute_jacobian",
+    "grad_hess_x",
+    "grad_hess_xu",
+    "quadratic_cost_derivs_diagonal",
+    "regularize_matrix",
+    "solve_psd",
     "BoxClampControl",
     "BoxTanhControl",
     "auxiliary_cost_derivs",

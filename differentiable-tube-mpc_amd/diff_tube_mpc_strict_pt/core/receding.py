@@ -35,6 +35,7 @@ class RecedingResult:
     collided: Tensor   # [B] bool
     status: Tensor     # [B] DTMPC_ST_* bits
     U_last: Tensor     # [B, N, 2] last (shifted) plan
+    iters: Optional[Tensor] = None  # [B] total iLQR iterations of each run (dtmpc_nominal_receding_it)
 
 
 def receding_setup_from_config(cfg: Dict[str, Any]) -> Tuple[DubinsDBaSProblem, QuadraticCost, ILQRConfig]:
@@ -81,15 +82,15 @@ def nominal_receding(*, problem: DubinsDBaSProblem, cost: QuadraticCost, cfg: IL
     xs = x0.t().contiguous()
     Us = to_soa(U_init.to(dt))
     log = torch.full((H, 6, B), math.nan, **kw)
-    ints = [torch.zeros(B, dtype=torch.int32, device=x0.device) for _ in range(4)]
+    ints = [torch.zeros(B, dtype=torch.int32, device=x0.device) for _ in range(5)]
     work = torch.empty(lib.dtmpc_receding_workspace_bytes(_dtype_code(x0), N, B), dtype=torch.uint8, device=x0.device)
-    _lib.check(lib.dtmpc_nominal_receding(_dtype_code(x0), C.byref(spec), C.byref(cc), C.byref(ic), B, int(H),
-                                          float(success_radius), xs.data_ptr(), Us.data_ptr(), log.data_ptr(),
-                                          *[t.data_ptr() for t in ints], work.data_ptr(), _lib.stream_of(x0)),
+    _lib.check(lib.dtmpc_nominal_receding_it(_dtype_code(x0), C.byref(spec), C.byref(cc), C.byref(ic), B, int(H),
+                                             float(success_radius), xs.data_ptr(), Us.data_ptr(), log.data_ptr(),
+                                             *[t.data_ptr() for t in ints], work.data_ptr(), _lib.stream_of(x0)),
                "dtmpc_nominal_receding")
-    h_ran, success_t, collided, status = ints
+    h_ran, success_t, collided, status, iters = ints
     if check:
         raise_for_status(status, "nominal_receding")
     lg = from_soa(log)
     return RecedingResult(x=lg[:, :, 0:3], u=lg[:, :, 3:5], b=lg[:, :, 5], h_ran=h_ran, success_t=success_t,
-                          collided=collided.bool(), status=status, U_last=from_soa(Us))
+                          collided=collided.bool(), status=status, U_last=from_soa(Us), iters=iters)

@@ -106,7 +106,7 @@ class TubeMPC:
     def __init__(self, setup, *, batch: int, device="cuda", dtype=torch.float32, disturbance: str = "philox",
                  seed: int = 0, global_offset: int = 0, global_batch: Optional[int] = None, process_group=None,
                  write_log: bool = False, record_choices: bool = False, grad_bound: Optional[float] = None,
-                 record_costs: bool = False):
+                 record_costs: bool = False, overlap: Optional[bool] = None):
         if isinstance(setup, dict):
             setup = paper_setup_from_config(setup)
         self.setup: PaperSetup = setup
@@ -154,7 +154,7 @@ class TubeMPC:
         self.Uaux = torch.zeros(N, 2, B, **kw)
         # lanes per trajectory and the fast kernel's launch chunk: resolved once here (DTMPC_TUBE_LANES and
         # DTMPC_FAST_CHUNK are read by the library only now), and the workspace sized for exactly these
-        self.lanes = int(self.lib.dtmpc_tube_lanes(B))
+        self.lanes = int(self.lib.dtmpc_tube_lanes_dtype(B, self._dt))  # the precision's own rule (ABI 6)
         self.chunk = int(self.lib.dtmpc_tube_chunk(N, self.lanes))
         wbytes = int(self.lib.dtmpc_tube_workspace_bytes(self._dt, N, B, self.lanes, self.chunk))
         if wbytes <= 0:
@@ -192,14 +192,37 @@ class TubeMPC:
         st.work_bytes = wbytes
         st.choices = self.choices.data_ptr() if self.choices is not None else None
         st.costs = self.costs.data_ptr() if self.costs is not None else None
+        st.phase = 0
         self.state = st
+        # overlap (the nominal solve is theta-independent, core/tube_mpc.py:723-728): each step runs
+        # as two launches (dtmpc_tube_state.phase 1: nominal, 2: the rest) and its theta all-reduce + update go to
+        # a side stream, which the NEXT step's phase 2 waits on -- so the collective overlaps the next nominal
+        # solve and never blocks the launch stream.  Default: on when the step has a cross-rank sum (a process
+        # group of > 1 ranks) and the fused kernel runs it in one chunk; overlap=True forces it (tests).
+        import torch.distributed as dist
+
+        multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
+        can = bool(self.lib.dtmpc_tube_split_supported(self._dt, C.byref(self.spec), C.byref(self.cfg))) and \
+            self.B <= self.chunk
+        if overlap and not can:
+            raise ValueError("overlap needs the fused tube kernel and B <= its launch chunk")
+        self.overlap = bool(can and (multi if overlap is None else overlap))
+        self._side = torch.cuda.Stream(device=self.device) if self.overlap else None
+        self._theta_ready = None  # event on the side stream: the last step's theta update is done
 
     # -----------------------------------------------------------------------------------------
+    def join(self) -> None:
+        """Make the current stream wait for the side stream's theta update (overlap mode): after it, theta,
+        vel and sums are the last step's on the current stream.  A no-op otherwise."""
+        if self._theta_ready is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._theta_ready)
+
     def reset(self, x0: Tensor, U_nom0: Optional[Tensor] = None, U_aux0: Optional[Tensor] = None) -> None:
         """x0 [B, 3]: plant and nominal start at x0, b0 = B(h(x0)) (core/tube_mpc.py:770-779);
         warm starts default to zero; theta and momentum restart from the setup."""
         if x0.shape != (self.B, 3):
             raise ValueError(f"x0 must be [{self.B}, 3]")
+        self.join()
         if U_nom0 is None and U_aux0 is None:
             # the whole episode start in one launch (dtmpc_tube_reset)
             x0c = x0.to(device=self.device, dtype=self.dtype).contiguous()
@@ -246,12 +269,31 @@ class TubeMPC:
             self.costs.fill_(float("nan"))
         if kernel_events is not None:
             kernel_events[0].record()
-        _lib.check(self.lib.dtmpc_tube_step(self._dt, C.byref(self.spec), C.byref(self.cfg), self.B,
-                                            self.global_offset, self.t, C.byref(self.state), wp, s),
-                   "dtmpc_tube_step")
+        if self.overlap:
+            self._launch(1, wp, s)  # the nominal solve: no theta (the side stream may still be updating it)
+            self.join()
+            self._launch(2, wp, s)
+        else:
+            self._launch(0, wp, s)
         if kernel_events is not None:
             kernel_events[1].record()
         if not adapt:
+            self.t += 1
+            return
+        if self.overlap:
+            _lib.check(self.lib.dtmpc_partials_reduce(self._dt, self.n_partials, self.partials.data_ptr(),
+                                                      self.sums.data_ptr(), s), "dtmpc_partials_reduce")
+            ready = torch.cuda.Event()
+            ready.record()
+            side = self._side
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                allreduce_sums(self.sums, self.group)  # RCCL's stream waits on `side`, `side` on the collective
+                _lib.check(self.lib.dtmpc_theta_update(self._dt, C.byref(self.adapt), 0.0, self.sums.data_ptr(),
+                                                       self.theta.data_ptr(), self.vel.data_ptr(),
+                                                       int(side.cuda_stream)), "dtmpc_theta_update")
+                self._theta_ready = torch.cuda.Event()
+                self._theta_ready.record(side)
             self.t += 1
             return
         _lib.check(self.lib.dtmpc_partials_reduce(self._dt, self.n_partials, self.partials.data_ptr(),
@@ -263,6 +305,12 @@ class TubeMPC:
                    "dtmpc_theta_update")
         self.t += 1
 
+    def _launch(self, phase: int, wp, s: int) -> None:
+        self.state.phase = phase
+        _lib.check(self.lib.dtmpc_tube_step(self._dt, C.byref(self.spec), C.byref(self.cfg), self.B,
+                                            self.global_offset, self.t, C.byref(self.state), wp, s),
+                   "dtmpc_tube_step")
+
     def check(self) -> None:
         raise_for_status(self.status, "tube step")
 
@@ -270,12 +318,14 @@ class TubeMPC:
     @property
     def loss_mean(self) -> float:
         """Mean upper loss of the last step over the healthy trajectories of the global batch."""
+        self.join()
         n = float(self.sums[_abi.TUBE_SUMS - 1])
         return float(self.sums[0]) / n if n > 0 else float("nan")
 
     @property
     def healthy_count(self) -> int:
         """Trajectories of the global batch that contributed to the last step's mean gradient."""
+        self.join()
         return int(round(float(self.sums[_abi.TUBE_SUMS - 1])))
 
     @property

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DTMPC_ABI_VERSION 5
+#define DTMPC_ABI_VERSION 6
 #define DTMPC_MAX_OBS 16
 #define DTMPC_MAX_ALPHAS 8
 #define DTMPC_MAX_HORIZON 512
@@ -172,7 +172,12 @@ typedef struct dtmpc_tube_state {
   int32_t* status;  /* [B] DTMPC_ST_* bits (OR-accumulated) */
   int32_t* iters;   /* [2][B] nominal / ancillary iterations used, or NULL */
   int32_t lanes;    /* lanes per trajectory, fixed when the state is built: dtmpc_tube_lanes(B) */
-  int32_t pad_;
+  int32_t phase;    /* ABI 6 (was padding, 0): which part of the step dtmpc_tube_step launches -- 0 the whole step;
+                       1 the nominal solve alone (theta-independent, core/tube_mpc.py:813-857); 2 the rest (the
+                       ancillary solve with the current theta, sensitivity, gradient sums, plant), after a phase-1
+                       launch of the same step on the same state.  Splitting lets a multi-rank caller run the
+                       previous step's theta all-reduce and update beside the nominal solve (TubeMPC, SURVEY.md
+                       §5); fused kernel only (dtmpc_tube_split_supported) */
   int64_t n_partials; /* rows of `partials`; must be >= dtmpc_tube_partials_count(B, lanes) */
   int64_t chunk;    /* trajectories per launch of the f32 fast kernel, fixed when the state is built:
                        dtmpc_tube_chunk(horizon, lanes) */
@@ -301,6 +306,11 @@ size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t
  * overrides.  Resolved ONCE, when the caller builds its state (dtmpc_tube_state.lanes);
  * dtmpc_tube_step never reads the environment. */
 int32_t dtmpc_tube_lanes(int64_t B);
+/* dtmpc_tube_lanes for a precision (ABI 6): DTMPC_F32 as dtmpc_tube_lanes; DTMPC_F64 4 while 4 B <= slots
+ * (B <= 16,384 on MI355X), else 1 -- the f64 step is instruction-bound, so the split line search pays for the
+ * duplicated recursion up to a quarter of the lane slots.  The default of dtmpc_ilqr_workspace_bytes /
+ * dtmpc_ilqr_solve_ws (lanes = 0) follows their dtype the same way.  0 for a bad dtype. */
+int32_t dtmpc_tube_lanes_dtype(int64_t B, int dtype);
 /* Number of per-workgroup partial records dtmpc_tube_step writes for B trajectories at `lanes`
  * lanes per trajectory (0 if lanes is not a supported count): one per workgroup of 256 threads, or of
  * 64 threads while B x lanes is below the device's wave slots (CUs x 4 SIMDs x 64). */
@@ -316,6 +326,9 @@ int64_t dtmpc_tube_partials_count(int64_t B, int32_t lanes);
 int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B,
                     int64_t global_offset, int64_t step, const dtmpc_tube_state* state,
                     const void* w, void* stream);
+/* 1 when dtmpc_tube_step runs the fused kernel for this problem / config / precision, which is what a phase
+ * split (dtmpc_tube_state.phase = 1, 2) needs; 0 otherwise.  Host-only. */
+int32_t dtmpc_tube_split_supported(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg);
 
 /* Episode start of the fused closed loop in one launch (core/tube_mpc.py:770-779; the reference's
  * run_closed_loop_experiment sets x = x_bar = x0, b = b_bar = B(h(x0)), zero warm starts and its
@@ -478,6 +491,13 @@ int dtmpc_nominal_receding(int dtype, const dtmpc_spec* spec, const dtmpc_cost* 
                            const dtmpc_ilqr_cfg* cfg, int64_t B, int32_t H, double success_radius,
                            const void* x0, void* U, void* log, int32_t* h_ran, int32_t* success_t,
                            int32_t* collided, int32_t* status, void* work, void* stream);
+/* dtmpc_nominal_receding with iters [B] out (ABI 6; may be NULL): each run's total iLQR iterations over its
+ * receding steps -- the receding leg of bench.py prices its algorithmic bytes by them (7,652 B
+ * per nominal iteration in f32). */
+int dtmpc_nominal_receding_it(int dtype, const dtmpc_spec* spec, const dtmpc_cost* cost,
+                              const dtmpc_ilqr_cfg* cfg, int64_t B, int32_t H, double success_radius,
+                              const void* x0, void* U, void* log, int32_t* h_ran, int32_t* success_t,
+                              int32_t* collided, int32_t* status, int32_t* iters, void* work, void* stream);
 
 #ifdef __cplusplus
 }

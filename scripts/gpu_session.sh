@@ -1,25 +1,25 @@
 #!/usr/bin/env bash
-# Round-4 GPU session (one gpurun call): smoke, the whole -m gpu suite with the parity prints (-s), then a
+# GPU session (one gpurun call): smoke, the whole -m gpu suite with the parity prints (-s), then a
 # short default bench line.  Every GPU step runs under its own time limit; a crash / timeout / abort ends
-# the session (pytest assertion failures, exit 1, do not).  Logs: gpurun_out/r04_<TAG>/.
-# usage: bash scripts/r04_session.sh TAG [steps: smoke tests bench] [pytest -k expression]
+# the session (pytest assertion failures, exit 1, do not).  Logs: gpurun_out/session_<TAG>/.
+# usage: bash scripts/gpu_session.sh TAG [steps: smoke tests bench] [pytest -k expression]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-s1}
 STEPS=${2:-"smoke tests bench"}
 KEXPR=${3:-}
-OUT=gpurun_out/r04_$TAG
+OUT=gpurun_out/session_$TAG
 mkdir -p "$OUT"
 run() {  # name seconds cmd...
   local name=$1 secs=$2
   shift 2
-  echo "[r04] $name: $*" | tee -a "$OUT/session.log"
+  echo "[gpu] $name: $*" | tee -a "$OUT/session.log"
   timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
-  echo "[r04] $name rc=$rc" | tee -a "$OUT/session.log"
+  echo "[gpu] $name rc=$rc" | tee -a "$OUT/session.log"
   tail -n 4 "$OUT/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
-    echo "[r04] stopping after $name (rc=$rc)" | tee -a "$OUT/session.log"
+    echo "[gpu] stopping after $name (rc=$rc)" | tee -a "$OUT/session.log"
     exit $rc
   fi
   return 0

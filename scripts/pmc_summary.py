@@ -87,6 +87,8 @@ def main():
             res["tube_step_bytes_per_launch"] = 1024.0 * (tube["FETCH_SIZE"] / rf + tube["WRITE_SIZE"] / rw)
             res["tube_step_read_bytes"] = 1024.0 * tube["FETCH_SIZE"] / rf
             res["tube_step_write_bytes"] = 1024.0 * tube["WRITE_SIZE"] / rw
+        # round 5: every leg's kernel (tube step, standalone iLQR, receding driver) under one key
+        res["kernel_bytes_per_launch"] = res["tube_step_bytes_per_launch"]
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -119,14 +119,15 @@ def test_arguments_validated_before_any_device_call(lib):
     # f32: the larger of the generic kernel's scratch (30 values per step) and the fast kernel's per-lane
     # records (two tapes of (N+1) x 16 B + N x 8 B, gains and sensitivity scratch of N x 40 B per
     # trajectory; four lanes: twelve tape slots per solve), for one launch chunk
-    per1, per4 = 51 * 32 + 50 * 96, 12 * (51 * 32 + 50 * 16) + 50 * 80
+    # (+ 12 B: the split step's hand-over of the nominal solve to its phase-2 launch, dtmpc_tube_state.phase, ABI 6)
+    per1, per4 = 51 * 32 + 50 * 96 + 12, 12 * (51 * 32 + 50 * 16) + 50 * 80 + 12
     c1, c4 = lib.dtmpc_tube_chunk(50, 1), lib.dtmpc_tube_chunk(50, 4)
     assert c1 == (0x7FFFFFFF // per1) // 256 * 256 and c4 == (0x7FFFFFFF // per4) // 256 * 256
     assert lib.dtmpc_tube_chunk(50, 3) == 0
     assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 65536, 1, c1) == max(4 * 50 * 30, per1) * 65536
     assert lib.dtmpc_tube_workspace_bytes(_abi.F32, 50, 4096, 4, c4) == per4 * 4096
     # f64 (csrc/dtmpc_fast64.hip): the same records in doubles, so twice the bytes and at most half the chunk
-    per1d, per4d = 2 * per1, 2 * per4
+    per1d, per4d = 2 * (per1 - 12) + 12, 2 * (per4 - 12) + 12
     c1d, c4d = (0x7FFFFFFF // per1d) // 256 * 256, (0x7FFFFFFF // per4d) // 256 * 256
     assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 65536, 1, c1) == max(8 * 50 * 30, per1d) * 65536
     assert lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, 4096, 4, c4) == per4d * 4096
@@ -146,6 +147,12 @@ def test_arguments_validated_before_any_device_call(lib):
     assert lib.dtmpc_general_partials_count(1000) == 4
     assert lib.dtmpc_tube_partials_count(1000, 4) == 63
     assert lib.dtmpc_tube_lanes(65536) in (1, 2, 4) and lib.dtmpc_tube_lanes(4096) in (1, 2, 4)
+    # ABI 6: the precision's rule (no device: the MI355X lane slots, 65,536) -- f32 as dtmpc_tube_lanes, f64 four
+    # lanes up to a quarter of the slots, then one
+    if not os.environ.get("DTMPC_TUBE_LANES"):
+        assert [lib.dtmpc_tube_lanes_dtype(b, 0) for b in (4096, 16384, 65536)] == [4, 2, 1]
+        assert [lib.dtmpc_tube_lanes_dtype(b, 1) for b in (4096, 16384, 32768, 65536)] == [4, 4, 1, 1]
+        assert lib.dtmpc_tube_lanes_dtype(4096, 7) == 0
     # the lane count and the partials size come from the state (resolved once by the caller)
     tc.aux_ilqr = st.ilqr_aux.to_c()
     for f in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux", "work", "theta", "partials", "status"):

@@ -29,7 +29,12 @@ NAMES = {
     "core.tube_mpc": ["run_closed_loop_experiment", "ExperimentTrajectories"],
     # core/__init__.py:9-20 (hot-path exports)
     "core": ["ILQRConfig", "SensitivityResult", "ilqr_solve", "ddp_sensitivity", "rollout", "IFTInputs",
-             "ift_gradient"],
+             "ift_gradient",
+             # core/__init__.py:22-31: the autograd fallbacks and the utils (round 5)
+             "grad_hess_xu", "grad_hess_x", "compute_jacobian", "solve_psd", "regularize_matrix",
+             "quadratic_cost_derivs_diagonal"],
+    "core.autodiff": ["grad_hess_xu", "grad_hess_x", "compute_jacobian"],
+    "core.utils": ["solve_psd", "regularize_matrix", "quadratic_cost_derivs_diagonal"],
     "core.ift": ["IFTInputs", "ift_gradient"],
     "core.ocp": ["rollout_dynamics", "total_cost"],
     "core.params": ["NominalTheta", "AuxiliaryTheta"],
@@ -65,3 +70,35 @@ def test_reference_dataclass_defaults():
         relaxed_inverse_barrier_B_alpha(torch.zeros(4), alpha=0.0)
     with pytest.raises(ValueError, match="no CPU fallback"):
         BoxClampControl(u_min=(-1.0, -1.0), u_max=(1.0, 1.0)).clamp(torch.zeros(2))
+
+
+def test_reference_utils_semantics():
+    """core.utils (core/utils.py:15-91) and core.autodiff (core/autodiff.py:9-82): plain torch helpers, checked
+    here on small CPU tensors against their closed forms (the device checks: tests/test_gpu_systems.py)."""
+    import torch
+
+    from diff_tube_mpc_strict_pt.core import (compute_jacobian, grad_hess_x, grad_hess_xu,
+                                              quadratic_cost_derivs_diagonal, regularize_matrix, solve_psd)
+
+    g = torch.Generator().manual_seed(0)
+    M = torch.randn(4, 4, generator=g, dtype=torch.float64)
+    A = M @ M.T + 0.1 * torch.eye(4, dtype=torch.float64)
+    b = torch.randn(4, 2, generator=g, dtype=torch.float64)
+    assert torch.allclose(A @ solve_psd(A, b), b, atol=1e-10)
+    assert torch.allclose(A @ solve_psd(A, b[:, 0]), b[:, 0], atol=1e-10)
+    S = torch.zeros(3, 3, dtype=torch.float64)  # singular: the regularised LU branch
+    assert torch.allclose(solve_psd(S, torch.ones(3, dtype=torch.float64), reg=0.5), torch.full((3,), 2.0, dtype=torch.float64))
+    assert torch.equal(regularize_matrix(S, 0.25), 0.25 * torch.eye(3, dtype=torch.float64))
+    x, u = torch.randn(4, generator=g, dtype=torch.float64), torch.randn(2, generator=g, dtype=torch.float64)
+    Q, R = torch.tensor([1.0, 2.0, 3.0, 0.5], dtype=torch.float64), torch.tensor([0.1, 0.2], dtype=torch.float64)
+    xr, ur = torch.randn(4, generator=g, dtype=torch.float64), torch.randn(2, generator=g, dtype=torch.float64)
+    ref = quadratic_cost_derivs_diagonal(x, u, Q, R, xr, ur)
+    auto = grad_hess_xu(lambda xx, uu, k: (Q * (xx - xr) ** 2).sum() + (R * (uu - ur) ** 2).sum(), x, u, 0)
+    for a, r in zip(auto, ref):
+        assert torch.allclose(a, r, atol=1e-12)
+    gx, Hx = grad_hess_x(lambda xx: (Q * xx ** 2).sum(), x)
+    assert torch.allclose(gx, 2 * Q * x) and torch.allclose(Hx, torch.diag(2 * Q))
+    Ja, Jb = compute_jacobian(lambda xx, uu: torch.stack([xx[0] + uu[0] * torch.cos(xx[2]), xx[1] * uu[1]]),
+                              x[:3], u)
+    assert torch.allclose(Ja, torch.tensor([[1.0, 0.0, -u[0] * torch.sin(x[2])], [0.0, u[1], 0.0]], dtype=torch.float64))
+    assert torch.allclose(Jb, torch.tensor([[torch.cos(x[2]), 0.0], [0.0, x[1]]], dtype=torch.float64))

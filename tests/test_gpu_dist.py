@@ -136,3 +136,34 @@ def test_two_rank_sharded_device_loop_matches_single_process(tmp_path, monkeypat
             # the batch sums, so those are not compared after step 0)
             err = np.abs(x_sh - full["x"][t]).max(0)
             assert (err < (1e-9 if f64 else 1e-4)).mean() > (0.99 if f64 else 0.97), (t, np.sort(err)[-5:])
+
+
+@pytest.mark.parametrize("lanes", ["4", "1"])
+@pytest.mark.parametrize("tag", ["f32", "f64"])
+def test_split_step_overlap_bitwise(monkeypatch, tag, lanes):
+    """TubeMPC(overlap=True) -- each step as two launches (dtmpc_tube_state.phase 1: nominal, 2: the rest) with the
+    theta all-reduce + update on a side stream that the next step's phase 2 waits on -- is the same computation as
+    the single launch: three closed-loop steps, every state array, theta, vel and the sums bitwise equal.  (One
+    process: allreduce_sums is the identity; the multi-rank path runs the same launches, RCCL unmeasured here.)"""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from diff_tube_mpc_strict_pt.core import TubeMPC
+
+    monkeypatch.setenv("DTMPC_TUBE_LANES", lanes)
+    dev = torch.device("cuda:0")
+    dt = torch.float64 if tag == "f64" else torch.float32
+    out = []
+    for ov in (False, True):
+        mpc = TubeMPC(_setup(), batch=1000, device=dev, dtype=dt, disturbance="philox", seed=SEED, overlap=ov,
+                      record_choices=True)
+        assert mpc.overlap == ov
+        mpc.reset(_x0(0, 1000))
+        for _ in range(3):
+            mpc.step()
+        mpc.join()
+        torch.cuda.synchronize(dev)
+        out.append({k: getattr(mpc, k).cpu().numpy().copy() for k in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux",
+                                                                       "Uaux", "theta", "vel", "sums", "status",
+                                                                       "iters", "choices")})
+    for k in out[0]:
+        assert np.array_equal(out[0][k], out[1][k], equal_nan=True), k

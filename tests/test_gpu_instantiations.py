@@ -88,17 +88,14 @@ def _truth(make, x0):
     return _snap(mpc)
 
 
-@pytest.mark.parametrize("m,g0", [(m, "") for m in range(1, 9)] + [(4, "0"), (5, "0"), (8, "0")])
+@pytest.mark.parametrize("m,g0", [(m, "") for m in range(1, 9)] + [(m, "0") for m in range(1, 9)])
 @pytest.mark.parametrize("tag", ["f64", "f32"])
-def test_tube_step_instantiations(dev, tag, m, g0, monkeypatch, request):
-    """g0 "0" (DTMPC_FAST_G0=0): the general gain records and recursion (tube_fast_kernel<M, P, 0>; the paper
-    mode's gamma is 0, so only this A/B switch reaches them), the f64 instantiations with the most scratch spill
-    traffic (up to 208 B per lane, hipcc -S).  Open defect: in f64 at M = 4 and 8 these
-    return non-finite statuses on some trajectories (M = 5 is correct) -- expected to fail, not reachable from a
-    product configuration (the switch is the only way in)."""
-    if tag == "f64" and g0 == "0" and m != 5:
-        request.node.add_marker(pytest.mark.xfail(reason="f64 general-record tube kernel at M != 5 (open defect)",
-                                                  strict=False))
+def test_tube_step_instantiations(dev, tag, m, g0, monkeypatch):
+    """g0 "0" (DTMPC_FAST_G0=0): the general gain records and recursion (tube_fast_kernel<M, P, 0>) on the paper
+    mode's gamma = 0 -- the kernels any setup with gamma != 0 runs (tests/test_gpu_general_records.py checks them
+    against the oracle at gamma = 0.3).  Round 4 had these failing in f64 at M = 4 and 8 (xfail); round 5 found the
+    cause in the f64 far-range sin / cos call's out-parameters and the kernels' scratch and
+    every f64 fused kernel now builds without a private segment (build.py check_resources)."""
     from diff_tube_mpc_strict_pt.core import TubeMPC
     from diff_tube_mpc_strict_pt.core.problem import paper_setup_from_config
 

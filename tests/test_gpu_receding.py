@@ -300,7 +300,8 @@ def test_reference_call_pattern(dev):
     assert float(phi_xx[3, 3]) == 2.0 * stage_cost.__self__.cost.qb
 
 
-@pytest.mark.parametrize("m,gamma,alpha", [(m, 0.0, 0.0) for m in range(1, 9)] + [(3, 0.3, 0.05), (8, 0.3, 0.05)])
+@pytest.mark.parametrize("m,gamma,alpha", [(m, 0.0, 0.0) for m in range(1, 9)] + [(3, 0.3, 0.05), (4, 0.3, 0.05),
+                                                                                (5, 0.3, 0.05), (8, 0.3, 0.05)])
 def test_receding_fused_instantiations_vs_generic(dev, oracle_lib, m, gamma, alpha):
     """The fused receding driver's other instantiations -- every obstacle count 1-8 (compile-time M) and the
     general gain records (gamma != 0, alpha > 0: receding_fast_kernel<M, 0>) -- against the generic kernel and

@@ -277,3 +277,36 @@ def test_autograd_through_per_function_api(dev, setting):
         nominal_cost_derivs_u(x_hat=xg, u=u_all[:4], target=(10.0, 10.0, 0.7), Q=(1.0, 1.0, 1.0), R=(1.0, 1.0), qb=1.0)
     with torch.no_grad():  # detached use stays allowed
         dubins_augmented_jacobian(xg, u_all[:4], cfg=dub, obs=obs, db_cfg=dbc, obs_beta=beta, obs_agg=st["agg"])
+
+
+@pytest.mark.parametrize("tag", ["f64", "f32"])
+def test_reference_autodiff_exports_on_device(dev, tag):
+    """core.compute_jacobian / grad_hess_xu / grad_hess_x (the reference's autograd fallbacks, core/autodiff.py:9-82,
+    re-exported in round 5) over the package's differentiable device functions: compute_jacobian of dubins_step at
+    the KAT points equals the library's analytic Jacobian (dubins_f_jac, itself checked against the reference's
+    KATs), and grad_hess_xu of a quadratic stage cost equals quadratic_cost_derivs_diagonal."""
+    from diff_tube_mpc_strict_pt.core import compute_jacobian, grad_hess_x, grad_hess_xu, quadratic_cost_derivs_diagonal
+    from diff_tube_mpc_strict_pt.core.systems.dubins import dubins_step
+    from diff_tube_mpc_strict_pt.core.systems.dubins_aug_jac import dubins_f_jac
+
+    npdt, tdt, tol = DT[tag]
+    k = golden(f"kat_{tag}")
+    dub, _, _, _ = _setup()
+    xh = torch.tensor(k["xh"], dtype=tdt, device=dev)
+    u = torch.tensor(k["u"], dtype=tdt, device=dev)
+    A, Bm = dubins_f_jac(xh[:, :3], u, cfg=dub)
+    for i in range(min(8, xh.shape[0])):
+        Ja, Jb = compute_jacobian(lambda x, uu: dubins_step(x, uu, cfg=dub), xh[i, :3], u[i])
+        assert Ja.device == dev
+        _close(Ja, A[i].cpu().numpy(), tol)
+        _close(Jb, Bm[i].cpu().numpy(), tol)
+    Q = torch.tensor([1.0, 2.0, 0.5, 3.0], dtype=tdt, device=dev)
+    R = torch.tensor([0.1, 0.2], dtype=tdt, device=dev)
+    xr = torch.tensor([10.0, 10.0, 0.7, 0.0], dtype=tdt, device=dev)
+    ref = quadratic_cost_derivs_diagonal(xh[0], u[0], Q, R, xr)
+    auto = grad_hess_xu(lambda x, uu, kk: (Q * (x - xr) ** 2).sum() + (R * uu ** 2).sum(), xh[0], u[0], 0)
+    for a, r in zip(auto, ref):
+        _close(a, r.cpu().numpy(), tol)
+    gx, Hx = grad_hess_x(lambda x: (Q * (x - xr) ** 2).sum(), xh[0])
+    _close(gx, ref[0].cpu().numpy(), tol)
+    _close(Hx, ref[2].cpu().numpy(), tol)
