@@ -410,6 +410,8 @@ def main() -> None:
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo rehearsal of launch, sharding and timing with a placeholder step (no GPU)")
     ap.add_argument("--no-steady", action="store_true", help="skip the free-running (warm-started) loop field")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: all-reduce theta in line instead of beside the next step's nominal solve (TubeMPC overlap)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary legs (f64 tube step, config-2 nominal DDP at B = 4096)")
     ap.add_argument("--workload", default="tube", choices=["tube", "nominal-ddp", "receding"],
@@ -469,7 +471,8 @@ def main() -> None:
             time.sleep(0.002)
     else:
         mpc = TubeMPC(setup, batch=hi - lo, device=dev, dtype=dtype, disturbance="philox", seed=0,
-                      global_offset=lo, global_batch=Bg, process_group=None)
+                      global_offset=lo, global_batch=Bg, process_group=None,
+                      overlap=False if args.no_overlap else None)
         x0 = initial_states(lo, hi, dev, dtype)
 
         def step(kernel_events=None):
@@ -579,6 +582,9 @@ def main() -> None:
             "global_batch": Bg, "batch_per_gpu": hi - lo, "horizon": setup.problem.horizon, "obstacles": 5,
             "line_search_alphas": len(setup.ilqr_nom.line_search_alphas), "parallelism": f"dp{world}",
         },
+        # N > 1: the step as two launches with the theta all-reduce + update on a side stream beside the next
+        # step's nominal solve (TubeMPC overlap); one process has no collective
+        "overlap": bool(mpc.overlap) if mpc is not None else False,
         "kernel_ms": kern_ms,
         "kernel_ms_max_over_ranks": kern_ms_max,
         "flagged_trajectories": int(cnt[0]),

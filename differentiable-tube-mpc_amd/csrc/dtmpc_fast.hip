@@ -85,9 +85,15 @@ constexpr int kTight = 16;
 // kWrap: the nominal target cost with the heading error wrapped to (-pi, pi] (run_nominal.py:297-324, the
 // receding-horizon driver's stage / terminal cost and derivatives); only the receding kernel sets it.
 constexpr int kWrap = 32;
-// kLds (f64): the obstacle table read from the workgroup's LDS copy at each use (obs_lds) instead of being held
-// in registers -- the f64 instantiations whose table cannot be pinned in VGPRs without spilling (tab_flag below)
+// kLds (f64): the obstacle table read again at each use instead of being held in registers -- the f64
+// instantiations whose table cannot be pinned in VGPRs without spilling (tab_flag below).  DTMPC_FAST64_TABSRC:
+// 1 (default) a scalar load of the kernarg segment's copy (every kernel's arguments start with its FP); 0 the
+// workgroup's LDS copy (obs_lds; A/B: at four lanes its even-M general-record kernels gave run-to-run
+// different results).
 constexpr int kLds = 64;
+#ifndef DTMPC_FAST64_TABSRC
+#define DTMPC_FAST64_TABSRC 1
+#endif
 template <int M>
 struct Obs {
   static constexpr int n = M & (kTight - 1);
@@ -96,38 +102,46 @@ struct Obs {
   static constexpr bool lds = (M & kLds) != 0;
 };
 
-#if DTMPC_FAST_F64
+#if DTMPC_FAST_F64 && DTMPC_FAST64_TABSRC == 0
 // the f64 kernels' obstacle table in LDS (x, y, r^2, -) per obstacle, written once per workgroup (obs_fill)
 __shared__ real obs_lds[32];
 #endif
-// obstacle i of the table: the registers of FP, or (kLds) the LDS copy, read through a volatile pointer so that
-// every use loads it again -- a hoisted load would hold the table in VGPRs for the whole loop, which is what kLds
-// instantiations cannot afford
+// obstacle i of the table: the registers of FP, or (kLds) loaded again at each use -- through an opaque pointer
+// (a hoisted load would hold the table in registers for the whole loop, which is what kLds instantiations cannot
+// afford): a scalar load from the kernarg segment (the value is wave-uniform, so it lands in an SGPR pair for the
+// few instructions that use it), or the LDS copy
+template <int M>
+__device__ __forceinline__ real otab_at(int f, int i) {
+#if DTMPC_FAST_F64 && DTMPC_FAST64_TABSRC == 0
+  return ((volatile __attribute__((address_space(3))) real*)obs_lds)[4 * i + f];
+#else
+  // kernarg FP: cx at offsetof(FP, cx), cy, r2 follow (f8 each); the pointer made opaque per use
+  typedef __attribute__((address_space(4))) const real creal;
+  creal* k = (creal*)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                      offsetof(FP, cx) + (unsigned)f * sizeof(f8));
+  __asm__ volatile("" : "+s"(k));
+  return k[i];
+#endif
+}
 template <int M>
 __device__ __forceinline__ real ocx(const FP& p, int i) {
-#if DTMPC_FAST_F64
-  if (Obs<M>::lds) return ((volatile __attribute__((address_space(3))) real*)obs_lds)[4 * i];
-#endif
+  if (DTMPC_FAST_F64 && Obs<M>::lds) return otab_at<M>(0, i);
   return p.cx[i];
 }
 template <int M>
 __device__ __forceinline__ real ocy(const FP& p, int i) {
-#if DTMPC_FAST_F64
-  if (Obs<M>::lds) return ((volatile __attribute__((address_space(3))) real*)obs_lds)[4 * i + 1];
-#endif
+  if (DTMPC_FAST_F64 && Obs<M>::lds) return otab_at<M>(1, i);
   return p.cy[i];
 }
 template <int M>
 __device__ __forceinline__ real or2(const FP& p, int i) {
-#if DTMPC_FAST_F64
-  if (Obs<M>::lds) return ((volatile __attribute__((address_space(3))) real*)obs_lds)[4 * i + 2];
-#endif
+  if (DTMPC_FAST_F64 && Obs<M>::lds) return otab_at<M>(2, i);
   return p.r2[i];
 }
 // kLds kernels: the table into LDS from the kernarg copy, before any lane returns (one barrier)
 template <int M>
 __device__ __forceinline__ void obs_fill(const FP& p) {
-#if DTMPC_FAST_F64
+#if DTMPC_FAST_F64 && DTMPC_FAST64_TABSRC == 0
   if (Obs<M>::lds) {
     if (threadIdx.x == 0) {
 #pragma unroll
@@ -1297,6 +1311,33 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
 #else
     ok = riccati_step(J, lx, lu, lxx, luu, reg, R, Kk, kk) && ok;
 #endif
+#ifdef DTMPC_FAST_DIAG_LANES
+    // diagnostics builds: the lanes of a trajectory must hold the same gains (they store the same record)
+    if (P > 1) {
+      int bad = -1;
+      real mine = 0, ref = 0;
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const real v = j < 8 ? Kk[j] : kk[j - 8];
+        const real r0 = gbc<P, 0>(v);
+        if (__builtin_bit_cast(unsigned long long, (double)v) != __builtin_bit_cast(unsigned long long, (double)r0)) {
+          bad = j;
+          mine = v;
+          ref = r0;
+        }
+      }
+      const real in[9] = {X.x, X.y, X.z, X.w, V.x, V.y, Lk.sn, Lk.gx, Lk.dB};
+      int badin = -1;
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+        if (__builtin_bit_cast(unsigned long long, (double)in[j]) !=
+            __builtin_bit_cast(unsigned long long, (double)gbc<P, 0>(in[j])))
+          badin = j;
+      if (bad >= 0 || badin >= 0)
+        printf("DIAG lanes blk=%d thr=%d h=%d k=%d gain=%d mine=%.17g lane0=%.17g input=%d\n", (int)blockIdx.x,
+               (int)threadIdx.x, h, k, bad, (double)mine, (double)ref, badin);
+    }
+#endif
     S.G.template store<SV::g0>(S.r, k, Kk, kk);
     gxn = Lk.gx;
     gyn = Lk.gy;
@@ -1497,6 +1538,7 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
     const f2 dy = C.a1[q] - ocy<M>(p, i);
     return ffma(dx, dx, dy * dy) - or2<M>(p, i);
   };
+  (void)hval;  // f32 keeps the h_i (only the f64 exp pass below evaluates them again)
 #pragma unroll
   for (int i = 0; i < MO; ++i) {
     const real cxi = ocx<M>(p, i), cyi = ocy<M>(p, i), r2i = or2<M>(p, i);  // one read per obstacle (kLds)
@@ -1942,10 +1984,17 @@ __device__ __forceinline__ void ls_stat(int trk, int best, real al, const FIlqr&
 // with the segment's copy at every phase boundary; the first lanes that disagree, or whose solve goes
 // non-finite, print where.  The general path forms its DBaS constants on the device, so only the table and the
 // dynamics constants are compared there.
+template <int MM>
 __device__ __forceinline__ void diag_p(const FP& p, int where, int it) {
   const FP* q = (const FP*)__builtin_amdgcn_kernarg_segment_ptr();
   int bad = -1;
   real v = 0, w = 0;
+#pragma unroll
+  for (int j = 0; j < Obs<MM>::n; ++j) {  // kLds: the LDS copy against the kernarg table
+    if (ocx<MM>(p, j) != q->cx[j]) { bad = 40 + j; v = ocx<MM>(p, j); w = q->cx[j]; }
+    if (ocy<MM>(p, j) != q->cy[j]) { bad = 50 + j; v = ocy<MM>(p, j); w = q->cy[j]; }
+    if (or2<MM>(p, j) != q->r2[j]) { bad = 60 + j; v = or2<MM>(p, j); w = q->r2[j]; }
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (__builtin_bit_cast(unsigned long long, (double)p.cx[j]) != __builtin_bit_cast(unsigned long long, (double)q->cx[j])) { bad = j; v = p.cx[j]; w = q->cx[j]; }
@@ -1961,9 +2010,9 @@ __device__ __forceinline__ void diag_p(const FP& p, int where, int it) {
     printf("DIAG const blk=%d thr=%d where=%d it=%d field=%d have=%.17g want=%.17g\n", (int)blockIdx.x,
            (int)threadIdx.x, where, it, bad, (double)v, (double)w);
 }
-#define DIAG_P(p, where, it) diag_p(p, where, it)
+#define DIAG_P(MM, p, where, it) diag_p<MM>(p, where, it)
 #else
-#define DIAG_P(p, where, it) ((void)0)
+#define DIAG_P(MM, p, where, it) ((void)0)
 #endif
 
 // P = 4 tape slots: slot q of the solve's X / U records at lane offset base + q * stride
@@ -2005,7 +2054,7 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
   int st = 0;
   int cur = kSlotInit;  // P = 4: the current tape's slot
   pf.mark(ph);
-  DIAG_P(p, TRACK ? 100 : 0, -1);
+  DIAG_P(M, p, TRACK ? 100 : 0, -1);
   for (int it = 0; it < cf.max_iter; ++it) {
     iters = it + 1;
     if (!backward<TRACK, M>(p, c, cf.reg, S, h)) {
@@ -2013,11 +2062,11 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
 #ifdef DTMPC_FAST_DIAG
       printf("DIAG backward non-finite blk=%d thr=%d h=%d trk=%d it=%d x0=(%.17g %.17g %.17g %.17g)\n", (int)blockIdx.x,
              (int)threadIdx.x, h, (int)TRACK, it, (double)x0[0], (double)x0[1], (double)x0[2], (double)x0[3]);
-      DIAG_P(p, TRACK ? 101 : 1, it);
+      DIAG_P(M, p, TRACK ? 101 : 1, it);
 #endif
       break;
     }
-    DIAG_P(p, TRACK ? 102 : 2, it);
+    DIAG_P(M, p, TRACK ? 102 : 2, it);
     pf.mark(ph + 1);
     real bestJ, al;
     int bc;
@@ -2042,11 +2091,11 @@ __device__ __forceinline__ int ilqr(const FP& p, const FCost& c, const FIlqr& cf
       printf("DIAG line search non-finite blk=%d thr=%d h=%d trk=%d it=%d Jprev=%.17g bestJ=%.17g x0=(%.17g %.17g %.17g %.17g)\n",
              (int)blockIdx.x, (int)threadIdx.x, h, (int)TRACK, it, (double)Jcur, (double)bestJ, (double)x0[0],
              (double)x0[1], (double)x0[2], (double)x0[3]);
-      DIAG_P(p, TRACK ? 103 : 3, it);
+      DIAG_P(M, p, TRACK ? 103 : 3, it);
 #endif
       break;
     }
-    DIAG_P(p, TRACK ? 104 : 4, it);
+    DIAG_P(M, p, TRACK ? 104 : 4, it);
     if (ch && h == 0) ch[it * chs] = (signed char)best;
     if (al != 0.f) {
       if (P == 4) {
@@ -2438,7 +2487,7 @@ tube_fast_kernel(FK kk) {
       const RA A8{K->a.oA8, cb * (32u * ES), l32}, A2{K->a.oA2, cb * (8u * ES), l8};
       const FP p = phase_p<ML>();
       st |= sensitivity<ML>(p, ca, Sa, A8, A2, acc);
-      DIAG_P(p, 200, st);
+      DIAG_P(ML, p, 200, st);
     }
     pf.mark(9);
     {  // plant step with disturbance, nominal propagation (:990-1001), log, warm-start shift
@@ -2496,7 +2545,7 @@ tube_fast_kernel(FK kk) {
         a.bbar[i] = qb;
       }
       acc[7] = 1.f;
-      DIAG_P(p, 300, st);
+      DIAG_P(ML, p, 300, st);
 #ifdef DTMPC_FAST_DIAG
       if (st && h == 0) printf("DIAG status traj=%d st=%d itn=%d ita=%d\n", i, st, itn, ita);
 #endif
@@ -3054,6 +3103,24 @@ bool FKN(tube_fast_eligible)(int dtype, const dtmpc_spec* sp, const dtmpc_tube_c
   return n.nc == FK_NS::NC && a.nc == FK_NS::NC;
 }
 
+// the record form a launch takes: 2 the compact gamma = 0 records and recursion (the default at gamma = 0), 1 the
+// compact records with the general recursion, 0 the general records; DTMPC_FAST_G0 = 0 / 1 (environment, read at
+// each call) lowers it for the A/B tests
+static int fast_g0(const dtmpc_spec* sp) {
+  int g0 = sp->dbas_gamma == 0.0 ? 2 : 0;
+  if (const char* e = getenv("DTMPC_FAST_G0"))
+    if ((e[0] == '0' || e[0] == '1') && e[1] == 0) g0 = g0 < e[0] - '0' ? g0 : e[0] - '0';
+  return g0;
+}
+
+#if DTMPC_FAST_F64
+// f64 at four lanes with the general records (gamma != 0): run-to-run different results and non-finite statuses on
+// some trajectories at some obstacle counts, moving with every change of the kernel's code (DESIGN.md section 9,
+// profiles/r05/f64_defect.txt) while the one- and two-lane forms and the compact-record four-lane form are correct
+// at every count -- dtmpc_tube_step runs that family on the generic f64 kernel instead
+bool tube_fast_lanes_ok64(const dtmpc_spec* sp, int lanes) { return !(lanes == 4 && fast_g0(sp) == 0); }
+#endif
+
 int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,
                      const dtmpc_tube_state* S, const void* w, hipStream_t st) {
   FK_NS::FK kk;
@@ -3099,9 +3166,10 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
   // barrier state's zero column (riccati_pk<true>).  DTMPC_FAST_G0 (environment, read at each call) = 0
   // keeps the general records and recursion, = 1 the compact records with the general recursion: the
   // tests compare 1 with 0 for exact equality (records) and the default with the oracle builds.
-  int g0 = kk.p.gamma == 0.f ? 2 : 0;
-  if (const char* e = getenv("DTMPC_FAST_G0"))
-    if ((e[0] == '0' || e[0] == '1') && e[1] == 0) g0 = g0 < e[0] - '0' ? g0 : e[0] - '0';
+  const int g0 = fast_g0(sp);
+#if DTMPC_FAST_F64
+  if (!tube_fast_lanes_ok64(sp, lanes)) return set_err(DTMPC_ERR_BAD_ARG, "f64 general records at four lanes run the generic kernel");
+#endif
   {
     const char* e = getenv("DTMPC_FAST_STAGGER");  // sleep rounds of ~8.1k cycles (A/B; default 0)
     a.stagger = e ? atoi(e) : 0;

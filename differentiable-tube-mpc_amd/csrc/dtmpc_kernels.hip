@@ -817,19 +817,21 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
   if (cfg->disturbance == 0 && !w) return set_err(DTMPC_ERR_BAD_ARG, "injected disturbance w is NULL");
   if (cfg->disturbance != 0 && cfg->disturbance != 1) return set_err(DTMPC_ERR_BAD_ARG, "bad disturbance mode");
   if (S->phase < 0 || S->phase > 2) return set_err(DTMPC_ERR_BAD_ARG, "state->phase must be 0, 1 or 2");
-  if (S->phase != 0 && !dtmpc_tube_split_supported(dtype, spec, cfg))
+  if (S->phase != 0 && !dtmpc_tube_split_supported(dtype, spec, cfg, S->lanes))
     return set_err(DTMPC_ERR_BAD_ARG, "a split step (state->phase 1 / 2) needs the fused kernel");
   hipStream_t st = (hipStream_t)stream;
   if (tube_fast_eligible(dtype, spec, cfg)) return launch_tube_fast(spec, cfg, B, global_offset, step, S, w, st);
-  if (tube_fast_eligible64(dtype, spec, cfg)) return launch_tube_fast64(spec, cfg, B, global_offset, step, S, w, st);
+  if (tube_fast_eligible64(dtype, spec, cfg) && tube_fast_lanes_ok64(spec, S->lanes))
+    return launch_tube_fast64(spec, cfg, B, global_offset, step, S, w, st);
   if (dtype == DTMPC_F32) return launch_tube<float>(spec, cfg, B, global_offset, step, S, w, st);
   if (dtype == DTMPC_F64) return launch_tube<double>(spec, cfg, B, global_offset, step, S, w, st);
   return set_err(DTMPC_ERR_BAD_ARG, "bad dtype");
 }
 
-int32_t dtmpc_tube_split_supported(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg) {
+int32_t dtmpc_tube_split_supported(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int32_t lanes) {
   if (!spec || !cfg) return 0;
-  return (tube_fast_eligible(dtype, spec, cfg) || tube_fast_eligible64(dtype, spec, cfg)) ? 1 : 0;
+  return (tube_fast_eligible(dtype, spec, cfg) ||
+          (tube_fast_eligible64(dtype, spec, cfg) && tube_fast_lanes_ok64(spec, lanes))) ? 1 : 0;
 }
 
 int dtmpc_partials_reduce(int dtype, int64_t n, const void* partials, void* sums, void* stream) {

@@ -207,7 +207,7 @@ PROTOTYPES = {
     "dtmpc_tube_workspace_bytes": (C.c_size_t, [C.c_int, I32, I64, I32, I64]),
     "dtmpc_tube_lanes": (I32, [I64]),
     "dtmpc_tube_lanes_dtype": (I32, [I64, C.c_int]),
-    "dtmpc_tube_split_supported": (I32, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcTubeCfg)]),
+    "dtmpc_tube_split_supported": (I32, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcTubeCfg), I32]),
     "dtmpc_tube_partials_count": (I64, [I64, I32]),
     "dtmpc_tube_step": (
         C.c_int,

@@ -202,7 +202,7 @@ class TubeMPC:
         import torch.distributed as dist
 
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
-        can = bool(self.lib.dtmpc_tube_split_supported(self._dt, C.byref(self.spec), C.byref(self.cfg))) and \
+        can = bool(self.lib.dtmpc_tube_split_supported(self._dt, C.byref(self.spec), C.byref(self.cfg), self.lanes)) and \
             self.B <= self.chunk
         if overlap and not can:
             raise ValueError("overlap needs the fused tube kernel and B <= its launch chunk")

@@ -326,9 +326,9 @@ int64_t dtmpc_tube_partials_count(int64_t B, int32_t lanes);
 int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B,
                     int64_t global_offset, int64_t step, const dtmpc_tube_state* state,
                     const void* w, void* stream);
-/* 1 when dtmpc_tube_step runs the fused kernel for this problem / config / precision, which is what a phase
- * split (dtmpc_tube_state.phase = 1, 2) needs; 0 otherwise.  Host-only. */
-int32_t dtmpc_tube_split_supported(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg);
+/* 1 when dtmpc_tube_step runs the fused kernel for this problem / config / precision and lane count, which is
+ * what a phase split (dtmpc_tube_state.phase = 1, 2) needs; 0 otherwise.  Host-only. */
+int32_t dtmpc_tube_split_supported(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int32_t lanes);
 
 /* Episode start of the fused closed loop in one launch (core/tube_mpc.py:770-779; the reference's
  * run_closed_loop_experiment sets x = x_bar = x0, b = b_bar = B(h(x0)), zero warm starts and its

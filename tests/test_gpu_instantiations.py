@@ -95,7 +95,11 @@ def test_tube_step_instantiations(dev, tag, m, g0, monkeypatch):
     mode's gamma = 0 -- the kernels any setup with gamma != 0 runs (tests/test_gpu_general_records.py checks them
     against the oracle at gamma = 0.3).  Round 4 had these failing in f64 at M = 4 and 8 (xfail); round 5 found the
     cause in the f64 far-range sin / cos call's out-parameters and the kernels' scratch and
-    every f64 fused kernel now builds without a private segment (build.py check_resources)."""
+    every f64 fused kernel now builds without a private segment (build.py check_resources).  f64 general records at
+    four lanes (this batch's own form) run the generic kernel (tube_fast_lanes_ok64), so the f64
+    "0" cases run the fused kernel at two lanes."""
+    if tag == "f64" and g0 == "0":
+        monkeypatch.setenv("DTMPC_TUBE_LANES", "2")
     from diff_tube_mpc_strict_pt.core import TubeMPC
     from diff_tube_mpc_strict_pt.core.problem import paper_setup_from_config
 

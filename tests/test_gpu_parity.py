@@ -160,6 +160,9 @@ def test_ilqr_ancillary_sensitivity_grad_vs_reference_golden(dev, oracle_lib, ta
 # costs tie at fp32 resolution near convergence, so even where the builds agree the device's decision
 # differs on a few percent of iLQR solves and on ~10 % of the 30-iteration tube steps (late iterations,
 # alpha = 0.01 vs keep); the f32 gates are set below those measurements, the rates are printed.
+# Round 4 added the stronger f32 gates (_f32_vs_truth: f64 truth + tie-aware decisions, >= 0.99 of trajectories);
+# these raw-rate gates stay as a second, weaker check of the same decision records (a regression floor on the
+# exact-match rate, whose f32 shortfall the tie-aware gate attributes to near-ties).
 DECISION_GATE = {"f64": 0.99, "f32": 0.95}
 DECISION_GATE_TUBE = {"f64": 0.99, "f32": 0.84}
 # the 20-iteration tracking solve with the tol exit compares tiny cost decreases (warm start next to the
@@ -828,11 +831,14 @@ def test_tube_step_fast_gamma0_records(dev, lanes, tag, monkeypatch):
     steps: states, tapes, log rows, partial sums and the shared theta.  DTMPC_FAST_G0=1 is the compact
     records with the general Riccati step; the default at gamma = 0 also drops the barrier state's zero
     column from the recursion (riccati_pk<true>, an FMA rounding of it), which test_tube_step_vs_oracle
-    checks against the oracle builds."""
+    checks against the oracle builds.  (f64 at four lanes: the general records run the generic f64 kernel,
+    tube_fast_lanes_ok64 -- there the two record forms are two different kernels and not compared bitwise.)"""
     import dataclasses
 
     from diff_tube_mpc_strict_pt.core import TubeMPC
 
+    if tag == "f64" and lanes == "4":
+        pytest.skip("f64 general records at four lanes run the generic kernel (DESIGN.md section 9)")
     monkeypatch.setenv("DTMPC_TUBE_LANES", lanes)
     st = paper_setup()
     assert st.problem.dbas_gamma == 0.0
