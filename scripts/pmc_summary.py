@@ -28,6 +28,9 @@ def _match(name, kern):
     return any(k in name for k in kern) if isinstance(kern, tuple) else kern in name
 
 
+SKIP = 0  # --skip N: drop each pass's first N dispatches of the kernel (a leg's warm-up launch of another size)
+
+
 def counters(root, kern, sub="*"):
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(root, sub, "run_counter_collection.csv")) + \
@@ -36,9 +39,11 @@ def counters(root, kern, sub="*"):
         for r in csv.DictReader(open(f)):
             if not _match(r["Kernel_Name"], kern):
                 continue
-            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+            per[(int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])
+        keep = sorted({d for d, _ in per})[SKIP:]
         for (d, c), v in per.items():
-            vals[c].append(v)
+            if d in keep:
+                vals[c].append(v)
     return {c: sum(v) / len(v) for c, v in vals.items()}
 
 
@@ -52,7 +57,9 @@ def kernel_stats(root, kern):
 
 
 def main():
+    global SKIP
     root, out = sys.argv[1], sys.argv[2]
+    SKIP = int(sys.argv[sys.argv.index("--skip") + 1]) if "--skip" in sys.argv else 0
     batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 65536
     # --kernel SUBSTR / --workload NAME: another kernel of the run, e.g. the f64 leg (fk64::tube_fast_kernel,
     # workload tube_f64: bench.py's tube_f64 roofline reads it; its record loads are all 16 B per lane, the
