@@ -111,6 +111,19 @@ def build(force: bool = False, variant: str = "", defines=(), only=(), on_produc
         if bad and os.environ.get("DTMPC_RESOURCE_STRICT", "1") != "0":
             raise RuntimeError("f64 fused kernels with a private segment (scratch): " +
                                ", ".join(f"{k} ({b} B)" for k, b in bad))
+        # and no 128-bit record store of a fused kernel may have its data registers written inside its two wait
+        # states (the store-data hazard, csrc/dtmpc_fast.hip st128; profiles/r05/store_hazard.txt)
+        haz = {}
+        for o in objs:
+            tu = os.path.basename(o).split(".")[0]
+            if tu.startswith("dtmpc_fast"):
+                haz[tu] = [list(h) for h in store_hazards(o)]
+        with open(os.path.join(CACHE, "store_hazards.json"), "w") as f:
+            json.dump(haz, f, indent=1, sort_keys=True)
+        nh = sum(len(v) for v in haz.values())
+        if nh and os.environ.get("DTMPC_RESOURCE_STRICT", "1") != "0":
+            raise RuntimeError(f"{nh} 128-bit stores with their data registers overwritten inside the hazard window "
+                               "(build/obj/store_hazards.json)")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -137,11 +150,7 @@ def kernel_resources(obj: str) -> dict:
     import tempfile
 
     with tempfile.TemporaryDirectory() as d:
-        fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "dev.co")
-        subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj, os.path.join(d, "x.o")],
-                       check=True, capture_output=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
-                        f"--targets=hipv4-amdgcn-amd-amdhsa--{ARCH}", f"--output={co}"], check=True, capture_output=True)
+        co = _code_object(obj, d)
         notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
                                text=True).stdout
     out, cur = {}, None
@@ -155,6 +164,68 @@ def kernel_resources(obj: str) -> dict:
             m = re.match(r"\s+\.%s:\s+(\d+)" % field, line)
             if m and cur is not None:
                 cur[key] = int(m.group(1))
+    return out
+
+
+def _code_object(obj: str, d: str) -> str:
+    fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "dev.co")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj, os.path.join(d, "x.o")],
+                   check=True, capture_output=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                    f"--targets=hipv4-amdgcn-amd-amdhsa--{ARCH}", f"--output={co}"], check=True, capture_output=True)
+    return co
+
+
+def _vregs(tok: str):
+    """The VGPR numbers of an operand token (v7, v[6:9])."""
+    import re
+
+    m = re.fullmatch(r"v(\d+)", tok) or re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
+    if not m:
+        return set()
+    lo = int(m.group(1))
+    hi = int(m.group(2)) if m.lastindex == 2 else lo
+    return set(range(lo, hi + 1))
+
+
+def store_hazards(obj: str) -> list:
+    """128-bit (and 96-bit) buffer stores whose data VGPRs a VALU instruction writes within the two wait states
+    after the store (the gfx950 store-data hazard the compiler does not pad for buffer stores with an SGPR soffset,
+    csrc/dtmpc_fast.hip st128): [(kernel, store line, offending line)] of the code object in a hipcc object."""
+    import re
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        co = _code_object(obj, d)
+        dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", f"--mcpu={ARCH}", "--no-show-raw-insn",
+                              "--no-leading-addr", co], check=True, capture_output=True, text=True).stdout
+    out, kern = [], None
+    lines = dis.splitlines()
+    for i, line in enumerate(lines):
+        m = re.match(r"^(\S+):$", line.strip()) if line and not line.startswith((" ", "\t")) else None
+        if m or re.match(r"^[0-9a-f]+ <(\S+)>:", line):
+            kern = (m.group(1) if m else re.match(r"^[0-9a-f]+ <(\S+)>:", line).group(1))
+            continue
+        t = line.split()
+        if not t or not re.match(r"buffer_store_dwordx[34]$", t[0]):
+            continue
+        data = _vregs(t[1].rstrip(","))
+        waits = 0
+        for nxt in lines[i + 1:i + 6]:
+            u = nxt.split()
+            if not u or u[0].endswith(":"):
+                break
+            if u[0] == "s_nop":
+                waits += int(u[1], 0) + 1
+            elif u[0].startswith("v_"):
+                if _vregs(u[1].rstrip(",")) & data:
+                    out.append((kern, line.strip(), nxt.strip()))
+                    break
+                waits += 1
+            else:
+                waits += 1
+            if waits >= 2:
+                break
     return out
 
 

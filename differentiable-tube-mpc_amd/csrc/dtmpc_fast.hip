@@ -91,6 +91,9 @@ constexpr int kWrap = 32;
 // workgroup's LDS copy (obs_lds; A/B: at four lanes its even-M general-record kernels gave run-to-run
 // different results).
 constexpr int kLds = 64;
+// kXasm (f64): the smooth-min exp's polynomial as one inline-assembly block (exp_sm<true>) -- set only where it
+// fits the register file without a private segment (xasm_flag below); elsewhere the same fmas compiled normally.
+constexpr int kXasm = 128;
 #ifndef DTMPC_FAST64_TABSRC
 #define DTMPC_FAST64_TABSRC 1
 #endif
@@ -100,6 +103,7 @@ struct Obs {
   static constexpr bool tight = (M & kTight) != 0;
   static constexpr bool wrap = (M & kWrap) != 0;
   static constexpr bool lds = (M & kLds) != 0;
+  static constexpr bool xasm = (M & kXasm) != 0;
 };
 
 #if DTMPC_FAST_F64 && DTMPC_FAST64_TABSRC == 0
@@ -280,6 +284,23 @@ struct RA {
 #ifndef DTMPC_FAST_STPOL
 #define DTMPC_FAST_STPOL 0  // cache-policy bits of the record stores (A/B)
 #endif
+// 128-bit buffer stores and the gfx950 store-data hazard (round 5).  A buffer_store_dwordx4 reads its data VGPRs
+// after issue; a VALU write to them in the next cycles changes what the store writes.  The compiler pads this hazard
+// only for stores without an SGPR soffset, and every record store here has one (the row base): it emitted a
+// dwordx4 store followed at once by a move into its data registers, and the store wrote the moved value
+// (profiles/r05/store_hazard.txt: one component of one record, a reproducible wrong tape).  DTMPC_FAST_STNOP = 1
+// (default): every 128-bit record store is followed by an s_nop 1 that reads its data registers, so they stay
+// unwritten for its two wait states.  Stores of 64 bits and less are not affected.
+#ifndef DTMPC_FAST_STNOP
+#define DTMPC_FAST_STNOP 1
+#endif
+template <class D>
+__device__ __forceinline__ void st128(D d, Rsrc r, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d), r, voff, soff, DTMPC_FAST_STPOL);
+#if DTMPC_FAST_STNOP
+  __asm__ volatile("s_nop 1" ::"v"(d));
+#endif
+}
 #if DTMPC_FAST_F64
 // f64: a 4-value row is 32 bytes (two 16-byte accesses), a 2-value row 16 bytes (one)
 typedef double d2v __attribute__((ext_vector_type(2)));
@@ -292,13 +313,10 @@ __device__ __forceinline__ f2 rld2(Rsrc r, const RA& a, int k, unsigned off) {
   return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off, a.so(k), 0));
 }
 __device__ __forceinline__ void rst4(Rsrc r, const RA& a, int k, unsigned off, f4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2v{v.x, v.y}), r, a.lo + off, a.so(k), DTMPC_FAST_STPOL);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, d2v{v.z, v.w}), r, a.lo + off + 16u, a.so(k),
-                                         DTMPC_FAST_STPOL);
+  st128(d2v{v.x, v.y}, r, a.lo + off, a.so(k));
+  st128(d2v{v.z, v.w}, r, a.lo + off + 16u, a.so(k));
 }
-__device__ __forceinline__ void rst2(Rsrc r, const RA& a, int k, unsigned off, f2 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, a.lo + off, a.so(k), DTMPC_FAST_STPOL);
-}
+__device__ __forceinline__ void rst2(Rsrc r, const RA& a, int k, unsigned off, f2 v) { st128(v, r, a.lo + off, a.so(k)); }
 #elif !defined(DTMPC_FAST_GLOBAL)
 __device__ __forceinline__ f4 rld4(Rsrc r, const RA& a, int k, unsigned off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off, a.so(k), 0));
@@ -306,9 +324,7 @@ __device__ __forceinline__ f4 rld4(Rsrc r, const RA& a, int k, unsigned off) {
 __device__ __forceinline__ f2 rld2(Rsrc r, const RA& a, int k, unsigned off) {
   return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, a.lo + off, a.so(k), 0));
 }
-__device__ __forceinline__ void rst4(Rsrc r, const RA& a, int k, unsigned off, f4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, a.lo + off, a.so(k), DTMPC_FAST_STPOL);
-}
+__device__ __forceinline__ void rst4(Rsrc r, const RA& a, int k, unsigned off, f4 v) { st128(v, r, a.lo + off, a.so(k)); }
 __device__ __forceinline__ void rst2(Rsrc r, const RA& a, int k, unsigned off, f2 v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v), r, a.lo + off, a.so(k), DTMPC_FAST_STPOL);
 }
@@ -408,8 +424,90 @@ __device__ __forceinline__ V ffma(V a, V b, V c) {
 // fdlibm kernels __kernel_sin / __kernel_cos on [-pi/4, pi/4] (< 1 ulp), the quadrant applied by exact
 // products with (A, B) in {0, +-1} as in the f32 form; |x| > 2^20 and non-finite take OCML sincos, out of
 // line (its Payne-Hanek branch would otherwise be inlined into every rollout step).
+// DTMPC_FAST64_EXP = 1: OCML's exp_f64 operation for operation (the same reduction, coefficients and fma order,
+// so bitwise the same values on [-1075, 1024]) without its two range selects -- every caller's argument is a
+// smooth-min exponent in [-50, 0] or NaN -- and with the polynomial's fmas in the three-address form
+// (v_fma_f64): the compiler otherwise emits each as a copy of the coefficient plus a two-address v_fmac_f64.
+#ifndef DTMPC_FAST64_EXP
+#define DTMPC_FAST64_EXP 3
+#endif
+template <bool ASM>
+__device__ __forceinline__ double exp_sm(double x) {
+  const double k = __builtin_rint(x * 0x1.71547652b82fep+0);
+  double r = __builtin_fma(-k, 0x1.62e42fefa39efp-1, x);
+  r = __builtin_fma(-k, 0x1.abc9e3b39803fp-56, r);
+  double q;
+  if (ASM) {
+  // the nine-fma Horner chain as one block: dependent v_fma_f64 need no wait states, and one block takes the
+  // compiler's conservative s_nop around inline assembly once instead of once per fma
+  __asm__("v_fma_f64 %0, %1, %2, %3\n\t"
+          "v_fma_f64 %0, %1, %0, %4\n\t"
+          "v_fma_f64 %0, %1, %0, %5\n\t"
+          "v_fma_f64 %0, %1, %0, %6\n\t"
+          "v_fma_f64 %0, %1, %0, %7\n\t"
+          "v_fma_f64 %0, %1, %0, %8\n\t"
+          "v_fma_f64 %0, %1, %0, %9\n\t"
+          "v_fma_f64 %0, %1, %0, %10\n\t"
+          "v_fma_f64 %0, %1, %0, %11"
+          : "=&v"(q)
+          : "v"(r), "v"(0x1.ade156a5dcb37p-26), "v"(0x1.28af3fca7ab0cp-22), "v"(0x1.71dee623fde64p-19),
+            "v"(0x1.a01997c89e6b0p-16), "v"(0x1.a01a014761f6ep-13), "v"(0x1.6c16c1852b7b0p-10),
+            "v"(0x1.1111111122322p-7), "v"(0x1.55555555502a1p-5), "v"(0x1.5555555555511p-3),
+            "v"(0x1.000000000000bp-1));
+  } else {
+  q = __builtin_fma(r, 0x1.ade156a5dcb37p-26, 0x1.28af3fca7ab0cp-22);
+  q = __builtin_fma(r, q, 0x1.71dee623fde64p-19);
+  q = __builtin_fma(r, q, 0x1.a01997c89e6b0p-16);
+  q = __builtin_fma(r, q, 0x1.a01a014761f6ep-13);
+  q = __builtin_fma(r, q, 0x1.6c16c1852b7b0p-10);
+  q = __builtin_fma(r, q, 0x1.1111111122322p-7);
+  q = __builtin_fma(r, q, 0x1.55555555502a1p-5);
+  q = __builtin_fma(r, q, 0x1.5555555555511p-3);
+  q = __builtin_fma(r, q, 0x1.000000000000bp-1);
+  }
+  q = __builtin_fma(r, q, 1.0);
+  q = __builtin_fma(r, q, 1.0);
+  return __builtin_ldexp(q, (int)k);
+}
+#ifdef DTMPC_DIAG_CHEAPEXP  // timing only (wrong results by design): exp through v_exp_f32
+__device__ __forceinline__ real vexp(real x) { return (double)__builtin_amdgcn_exp2f((float)(x * 1.4426950408889634)); }
+#elif DTMPC_FAST64_EXP
+__device__ __forceinline__ real vexp(real x) { return exp_sm<false>(x); }
+#else
 __device__ __forceinline__ real vexp(real x) { return m_exp(x); }
-__device__ __forceinline__ f2 vexp(f2 x) { return f2{m_exp(x.x), m_exp(x.y)}; }
+#endif
+__device__ __forceinline__ f2 vexp(f2 x) { return f2{vexp(x.x), vexp(x.y)}; }
+// 1 / x and a / b for the call sites whose divisor is a finite positive normal or NaN (the barrier's max(z, eps),
+// the smooth-min sum se in [1, M], the log's 2 + f in [1.4, 2.9]).  DTMPC_FAST64_RCP = 1: v_rcp_f64 (~2^-23
+// relative) and two Newton steps (1 / x within an ulp); the quotient a r corrected by one residual step, i.e. 5 and
+// 6 instructions against IEEE division's 11 (div_scale, div_fmas, div_fixup).  0: IEEE division.
+#ifndef DTMPC_FAST64_HGLOG
+#define DTMPC_FAST64_HGLOG 1
+#endif
+#ifndef DTMPC_FAST64_RCP
+#define DTMPC_FAST64_RCP 1
+#endif
+__device__ __forceinline__ real frcp(real x) {
+#if DTMPC_FAST64_RCP
+  double r = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-x, r, 1.0);
+  return __builtin_fma(r, e, r);
+#else
+  return 1.0 / x;
+#endif
+}
+__device__ __forceinline__ real fdiv(real a, real b) {
+#if DTMPC_FAST64_RCP
+  double r = __builtin_amdgcn_rcp(b);
+  r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+  const double q = a * r;
+  return __builtin_fma(r, __builtin_fma(-b, q, a), q);
+#else
+  return a / b;
+#endif
+}
 // the smooth-min log log(se), se in [1, M] (its largest term is exp(0)): fdlibm's e_log -- frexp, s = f / (2 + f),
 // a degree-14 odd polynomial in s (< 1 ulp), ~35 instructions against OCML's ~90 (a double-double evaluation);
 // +inf passes through.  Measured: f64 tube step 14.72 -> 13.90 ms at B = 65,536 (profiles/r03/f64_log_experiment.txt)
@@ -424,7 +522,7 @@ __device__ __forceinline__ real vlog(real x) {
     m = m + m;
     e = e - 1;
   }
-  const double k = (double)e, f = m - 1.0, s = f / (2.0 + f), z = s * s, w = z * z;
+  const double k = (double)e, f = m - 1.0, s = fdiv(f, 2.0 + f), z = s * s, w = z * z;
   const double t1 = w * __builtin_fma(w, __builtin_fma(w, Lg6, Lg4), Lg2);
   const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, Lg7, Lg5), Lg3), Lg1);
   const double R = t2 + t1, hfsq = 0.5 * f * f;
@@ -444,15 +542,27 @@ __device__ __forceinline__ V smarg(const FP& p, V hi, V zmax) {
   DTMPC_NOCONTRACT
   return p.neg_beta * hi - zmax;
 }
+#if DTMPC_FAST64_EXP
+// branch-free: the caller's wave-uniform branch already decided that some lane needs this term; exp_sm of an
+// argument below -50 (down to -inf) is a finite number, 0 or NaN and is replaced by 0
+template <int M = 0>
+__device__ __forceinline__ real smexp(real x) {
+  const real e = exp_sm<Obs<M>::xasm && DTMPC_FAST64_EXP == 3>(x);
+  return x < -kSmSkip ? 0.0 : e;
+}
+#else
+template <int M = 0>
 __device__ __forceinline__ real smexp(real x) { return x < -kSmSkip ? 0.0 : vexp(x); }
-__device__ __forceinline__ f2 smexp(f2 x) { return f2{smexp(x.x), smexp(x.y)}; }
+#endif
+template <int M = 0>
+__device__ __forceinline__ f2 smexp(f2 x) { return f2{smexp<M>(x.x), smexp<M>(x.y)}; }
 __device__ __forceinline__ bool smneed(real x) { return !(x < -kSmSkip); }  // NaN: needed (it propagates)
 __device__ __forceinline__ bool smneed(f2 x) { return smneed(x.x) || smneed(x.y); }
-template <class V>
+template <int M = 0, class V>
 __device__ __forceinline__ V smterm(const FP& p, V hi, V zmax, V) {
   const V x = smarg(p, hi, zmax);
   V e = V(0.0);
-  if (__builtin_amdgcn_ballot_w64(smneed(x))) e = smexp(x);  // wave-uniform
+  if (__builtin_amdgcn_ballot_w64(smneed(x))) e = smexp<M>(x);  // wave-uniform
   return e;
 }
 #ifndef DTMPC_FAST_SINCOS_AB
@@ -554,8 +664,9 @@ __device__ __forceinline__ f2 vexp2(f2 x) { return f2{__builtin_amdgcn_exp2f(x.x
 __device__ __forceinline__ f2 vexp(f2 x) { return pk_exp(x); }
 __device__ __forceinline__ real vlog(real x) { return m_log(x); }
 __device__ __forceinline__ f2 vlog(f2 x) { return pk_log(x); }
+__device__ __forceinline__ real frcp(real x) { return m_rcp(x); }
 // the smooth-min term exp(-beta h_i - zmax) = exp2(fma(h_i, -beta log2(e), -zmax log2(e))) (zl = zmax log2 e)
-template <class V>
+template <int M = 0, class V>
 __device__ __forceinline__ V smterm(const FP& p, V hi, V, V zl) {
   return vexp2(__builtin_elementwise_fma(hi, V(p.nbl2e), -zl));
 }
@@ -614,13 +725,13 @@ __device__ __forceinline__ real bar_relaxed(const FP& p, real z) {
 // 1 / max(z, eps) with max NaN-propagating (= the reference's torch.clamp_min then reciprocal)
 __device__ __forceinline__ real vbarrier(const FP& p, real z) {
   DTMPC_NOCONTRACT
-  real r = m_rcp(vmaxnan(z, p.eps));
+  real r = frcp(vmaxnan(z, p.eps));
   if (!(z >= p.a)) r = bar_relaxed(p, z);
   return r;
 }
 __device__ __forceinline__ f2 vbarrier(const FP& p, f2 z) {
   DTMPC_NOCONTRACT
-  f2 r = f2{m_rcp(vmaxnan(z.x, p.eps)), m_rcp(vmaxnan(z.y, p.eps))};
+  f2 r = f2{frcp(vmaxnan(z.x, p.eps)), frcp(vmaxnan(z.y, p.eps))};
   if (!(z.x >= p.a) || !(z.y >= p.a)) {
     if (!(z.x >= p.a)) r.x = bar_relaxed(p, z.x);
     if (!(z.y >= p.a)) r.y = bar_relaxed(p, z.y);
@@ -654,7 +765,7 @@ __device__ __forceinline__ V h_sm(const FP& p, V px, V py) {
   const V zl = zmax * real(1.44269504088896341);
   V se = 0.f;
 #pragma unroll
-  for (int i = 0; i < MO; ++i) se += smterm(p, hi[i], zmax, zl);
+  for (int i = 0; i < MO; ++i) se += smterm<M>(p, hi[i], zmax, zl);
   const V hv = p.neg_inv_beta * (zmax + vlog(se));
   return Obs<M>::tight ? hv - p.tight : hv;  // kTight: the tightened h the barrier sees
 }
@@ -702,7 +813,7 @@ __device__ __forceinline__ real h_grad(const FP& p, real px, real py, real& gx, 
     // the generic kernel's h_grad (dtmpc_device.hpp), with the smooth-min's rule for negligible terms (smterm)
     const real x = zi - zmax;
     real e = 0.0;
-    if (__builtin_amdgcn_ballot_w64(smneed(x))) e = smexp(x);
+    if (__builtin_amdgcn_ballot_w64(smneed(x))) e = smexp<M>(x);
 #else
     (void)zi;
     const real e = __builtin_amdgcn_exp2f(__builtin_fmaf(hh[TWO ? 0 : i], p.nbl2e, -zl));
@@ -711,12 +822,16 @@ __device__ __forceinline__ real h_grad(const FP& p, real px, real py, real& gx, 
     sx += e * (2.f * dx);  // = 2 (px - cx_i), the first loop's difference
     sy += e * (2.f * dy);
   }
-  const real inv = m_rcp(se);
+  const real inv = frcp(se);
   gx = sx * inv;
   gy = sy * inv;
   // untightened also under kTight: the reference linearises the nominal with dubins_augmented_jacobian of
   // the plain h (core/tube_mpc.py:315-320) while its dynamics see h - s (:273-276); dtmpc_solver.hpp alike
+#if DTMPC_FAST_F64 && DTMPC_FAST64_HGLOG
+  return p.neg_inv_beta * (zmax + vlog(se));  // the line search's log (fdlibm, < 1 ulp) instead of OCML's
+#else
   return p.neg_inv_beta * (zmax + m_log(se));
+#endif
 }
 
 // DBaS-augmented Dubins step (fhat_vec): x' = dubins_step(x, u) (core/systems/dubins.py:26-45),
@@ -1228,6 +1343,12 @@ __device__ __forceinline__ Lin lin_point(const FP& p, const f4& X) {
 // trajectory, and handed to every lane by DPP broadcasts; the Riccati recursion itself is sequential
 // and runs on every lane (each needs the gains).  Same operations on the same values as P = 1: the
 // gains are bitwise those of the one-lane form.
+#ifndef DTMPC_FAST_BW_OPQ
+#define DTMPC_FAST_BW_OPQ 1
+#endif
+#ifndef DTMPC_FAST_BW_BCAST
+#define DTMPC_FAST_BW_BCAST 1
+#endif
 template <bool TRACK, int M, class SV>
 __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, const SV& S, int h) {
   constexpr int P = SV::lanes;
@@ -1277,10 +1398,11 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
   real gxn, gyn;
   real dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
   bool ok = finite(RVX(0)) && finite(RVX(1)) && finite(RVX(2)) && finite(RVX(3));
-  // step inputs one step ahead
-  f4 nX = S.x(N - 1), nR = f4{0.f, 0.f, 0.f, 0.f};
-  f2 nV = S.u(N - 1), nQ = f2{0.f, 0.f};
-  if (TRACK) {
+  // step inputs one step ahead (P > 1 with BW_BCAST: from the group's per-lane rows instead)
+  constexpr bool BCI = P > 1 && DTMPC_FAST_BW_BCAST != 0;
+  f4 nX = BCI ? f4{0.f, 0.f, 0.f, 0.f} : S.x(N - 1), nR = f4{0.f, 0.f, 0.f, 0.f};
+  f2 nV = BCI ? f2{0.f, 0.f} : S.u(N - 1), nQ = f2{0.f, 0.f};
+  if (TRACK && !BCI) {
     nR = S.xr(N - 1);
     nQ = S.ur(N - 1);
   }
@@ -1368,18 +1490,68 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
       const int r = kt - h > 0 ? kt - h : 0;
       return rld4(S.r, S.XA, uidx(rb), (unsigned)(r - rb) * S.XA.rs);
     };
-    f4 PX = prow(N - 1);
+    // BW_BCAST: the step inputs too -- lane h reads the controls (and the ancillary's reference rows) of row kt - h
+    // one group ahead, and every step takes row k's values from lane kt - k by the same DPP broadcasts instead of
+    // reading them one step ahead (a group of P steps of load latency covered instead of one)
+    auto prow2 = [&](const RA& A, int kt) {
+      const int rb = kt - (P - 1) > 0 ? kt - (P - 1) : 0;
+      const int r = kt - h > 0 ? kt - h : 0;
+      return rld2(S.r, A, uidx(rb), (unsigned)(r - rb) * A.rs);
+    };
+    auto prow4 = [&](const RA& A, int kt) {
+      const int rb = kt - (P - 1) > 0 ? kt - (P - 1) : 0;
+      const int r = kt - h > 0 ? kt - h : 0;
+      return rld4(S.r, A, uidx(rb), (unsigned)(r - rb) * A.rs);
+    };
+    constexpr bool BC = DTMPC_FAST_BW_BCAST != 0;
+    f4 PX = prow(N - 1), PR = f4{0.f, 0.f, 0.f, 0.f};
+    f2 PV = f2{0.f, 0.f}, PQ = f2{0.f, 0.f};
+    if (BC) {
+      PV = prow2(S.UA, N - 1);
+      if (TRACK) {
+        PR = prow4(S.XRA, N - 1);
+        PQ = prow2(S.URA, N - 1);
+      }
+    }
     for (int kt = N - 1; kt >= 0; kt -= P) {
-      const f4 PXc = PX;
-      if (kt - P >= 0) PX = prow(kt - P);
+      const f4 PXc = PX, PRc = PR;
+      const f2 PVc = PV, PQc = PQ;
+      if (kt - P >= 0) {
+        PX = prow(kt - P);
+        if (BC) {
+          PV = prow2(S.UA, kt - P);
+          if (TRACK) {
+            PR = prow4(S.XRA, kt - P);
+            PQ = prow2(S.URA, kt - P);
+          }
+        }
+      }
       const Lin Lh = lin_point<M>(p, PXc);
 #pragma unroll
       for (int j = 0; j < P; ++j) {
         const int k = kt - j;
         if (k < 0) break;
-        const f4 X = nX, Rr = nR;
-        const f2 V = nV, Q = nQ;
-        next_inputs(k);
+        f4 X = nX, Rr = nR;
+        f2 V = nV, Q = nQ;
+        if (BC) {
+          // each broadcast value made opaque, as a loaded value is: the step's arithmetic then compiles as in the
+          // load form (the same FMA contraction of the Riccati step, so the same gains bit for bit)
+          auto bq = [&](real v) {
+            real w = gbcast<P>(v, j);
+#if DTMPC_FAST_BW_OPQ
+            __asm__("" : "+v"(w));
+#endif
+            return w;
+          };
+          X = f4{bq(PXc.x), bq(PXc.y), bq(PXc.z), bq(PXc.w)};
+          V = f2{bq(PVc.x), bq(PVc.y)};
+          if (TRACK) {
+            Rr = f4{bq(PRc.x), bq(PRc.y), bq(PRc.z), 0.f};
+            Q = f2{bq(PQc.x), bq(PQc.y)};
+          }
+        } else {
+          next_inputs(k);
+        }
         Lin Lk;
         Lk.sn = gbcast<P>(Lh.sn, j);
         Lk.cs = gbcast<P>(Lh.cs, j);
@@ -1420,19 +1592,10 @@ struct Cand {
   f2 a0[NPR], a1[NPR], a2[NPR], ab[NPR], Bp[NPR], J[NPR], al[NPR];
 };
 
-// sin / cos of NPR pairs (pk_sincos per pair); one range test for all of them
+#if !DTMPC_FAST_F64 && !defined(DTMPC_OCML_SINCOS)
+// sin / cos of NPR pairs whose elements are all in [-65536, 65536] (no range test, no branch)
 template <int NPR>
-__device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
-#if DTMPC_FAST_F64
-#pragma unroll
-  for (int q = 0; q < NPR; ++q) vsincos(x[q], sn[q], cs[q]);
-}
-#else
-  real m = __builtin_fabsf(x[0].x);
-#pragma unroll
-  for (int q = 0; q < NPR; ++q) m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(x[q].x), __builtin_fabsf(x[q].y)));
-#ifndef DTMPC_OCML_SINCOS
-  if (__builtin_expect(m <= 65536.0f, 1)) {
+__device__ __forceinline__ void sincos_pairs_fast(const f2* x, f2* sn, f2* cs) {
     f2 qq[NPR], r[NPR], z[NPR], s[NPR], c[NPR];
 #pragma unroll
     for (int q = 0; q < NPR; ++q) qq[q] = f2{__builtin_rintf(x[q].x * k2oPi), __builtin_rintf(x[q].y * k2oPi)};
@@ -1478,6 +1641,22 @@ __device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
       cs[q] = f2{((j0 + 1) & 2) ? -co0 : co0, ((j1 + 1) & 2) ? -co1 : co1};
     }
 #endif
+}
+#endif
+// sin / cos of NPR pairs (pk_sincos per pair); one range test for all of them
+template <int NPR>
+__device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
+#if DTMPC_FAST_F64
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) vsincos(x[q], sn[q], cs[q]);
+}
+#else
+  real m = __builtin_fabsf(x[0].x);
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(x[q].x), __builtin_fabsf(x[q].y)));
+#ifndef DTMPC_OCML_SINCOS
+  if (__builtin_expect(m <= 65536.0f, 1)) {
+    sincos_pairs_fast<NPR>(x, sn, cs);
     return;
   }
 #endif
@@ -1491,6 +1670,87 @@ __device__ __forceinline__ void sincos_pairs(const f2* x, f2* sn, f2* cs) {
   }
 }
 #endif
+
+// B(h(x)) of NPR pairs of positions (the line search's DBaS barrier; relaxed inverse barrier of the smooth-min h)
+template <int M, int NPR>
+__device__ __forceinline__ void ls_bar(const FP& p, const f2* px, const f2* py, f2* Bn) {
+  DTMPC_NOCONTRACT
+  // smooth-min h over the M obstacles (h_sm), all pairs together.  TWO (kLds, f64): the h_i are not kept between
+  // the min and the exp pass but evaluated again (the same operations, so bitwise the same values) -- at M = 8
+  // the kept 8 x NPR pairs of doubles were what made the general-record kernels spill (build.py check_resources)
+  constexpr int MO = Obs<M>::n;
+  constexpr bool TWO = Obs<M>::lds;
+  f2 hi[TWO ? 1 : MO][NPR], hm[NPR];
+  auto hval = [&](int i, int q) {
+    const f2 dx = px[q] - ocx<M>(p, i);
+    const f2 dy = py[q] - ocy<M>(p, i);
+    return ffma(dx, dx, dy * dy) - or2<M>(p, i);
+  };
+  (void)hval;  // f32 keeps the h_i (only the f64 exp pass below evaluates them again)
+#pragma unroll
+  for (int i = 0; i < MO; ++i) {
+    const real cxi = ocx<M>(p, i), cyi = ocy<M>(p, i), r2i = or2<M>(p, i);  // one read per obstacle (kLds)
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      const f2 dx = px[q] - cxi;
+      const f2 dy = py[q] - cyi;
+      const f2 h = ffma(dx, dx, dy * dy) - r2i;
+      if (!TWO) hi[i][q] = h;
+      hm[q] = i == 0 ? h : vmin(hm[q], h);
+    }
+  }
+  f2 zmax[NPR], zl[NPR], se[NPR], z[NPR];
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    zmax[q] = p.neg_beta * hm[q];
+    zl[q] = zmax[q] * real(1.44269504088896341);
+  }
+#pragma unroll
+  for (int i = 0; i < MO; ++i) {
+#if DTMPC_FAST_F64
+    // one wave-uniform branch per obstacle for all the lane's candidates (smterm)
+    f2 x[NPR], e[NPR];
+    bool need = false;
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      x[q] = smarg(p, TWO ? hval(i, q) : hi[TWO ? 0 : i][q], zmax[q]);
+      need = need || smneed(x[q]);
+      e[q] = f2(0.0);
+    }
+    if (__builtin_amdgcn_ballot_w64(need))
+#pragma unroll
+      for (int q = 0; q < NPR; ++q) e[q] = smexp<M>(x[q]);
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) se[q] = i == 0 ? e[q] : se[q] + e[q];
+#else
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      const f2 e = smterm<M>(p, hi[TWO ? 0 : i][q], zmax[q], zl[q]);
+      se[q] = i == 0 ? e : se[q] + e;  // = 0 + e_0 + ...: e_0 >= 0, so 0 + e_0 == e_0 bitwise
+    }
+#endif
+  }
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    z[q] = p.neg_inv_beta * (zmax[q] + vlog(se[q]));
+    if (Obs<M>::tight) z[q] = z[q] - p.tight;
+  }
+  // relaxed inverse barrier: the reciprocal for every element, the quadratic branch (z < a) once
+  // per step for whichever elements need it
+  real zmin = z[0].x;
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    Bn[q] = f2{frcp(vmaxnan(z[q].x, p.eps)), frcp(vmaxnan(z[q].y, p.eps))};
+    zmin = m_min(zmin, m_min(z[q].x, z[q].y));
+  }
+  if (!(zmin >= p.a)) {
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      if (!(z[q].x >= p.a)) Bn[q].x = bar_relaxed(p, z[q].x);
+      if (!(z[q].y >= p.a)) Bn[q].y = bar_relaxed(p, z[q].y);
+    }
+  }
+}
 
 // one step of the NPR pairs' rollouts: feedback + clamp, stage cost, DBaS-augmented Dubins move
 template <bool TRACK, int M, int NPR, bool G0>
@@ -1527,82 +1787,8 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
     C.a1[q] = ffma(dv, sn[q], C.a1[q]);
     C.a2[q] = ffma(f2(p.dt), u1[q], C.a2[q]);
   }
-  // smooth-min h over the M obstacles (h_sm), all pairs together.  TWO (kLds, f64): the h_i are not kept between
-  // the min and the exp pass but evaluated again (the same operations, so bitwise the same values) -- at M = 8
-  // the kept 8 x NPR pairs of doubles were what made the general-record kernels spill (build.py check_resources)
-  constexpr int MO = Obs<M>::n;
-  constexpr bool TWO = Obs<M>::lds;
-  f2 hi[TWO ? 1 : MO][NPR], hm[NPR];
-  auto hval = [&](int i, int q) {
-    const f2 dx = C.a0[q] - ocx<M>(p, i);
-    const f2 dy = C.a1[q] - ocy<M>(p, i);
-    return ffma(dx, dx, dy * dy) - or2<M>(p, i);
-  };
-  (void)hval;  // f32 keeps the h_i (only the f64 exp pass below evaluates them again)
-#pragma unroll
-  for (int i = 0; i < MO; ++i) {
-    const real cxi = ocx<M>(p, i), cyi = ocy<M>(p, i), r2i = or2<M>(p, i);  // one read per obstacle (kLds)
-#pragma unroll
-    for (int q = 0; q < NPR; ++q) {
-      const f2 dx = C.a0[q] - cxi;
-      const f2 dy = C.a1[q] - cyi;
-      const f2 h = ffma(dx, dx, dy * dy) - r2i;
-      if (!TWO) hi[i][q] = h;
-      hm[q] = i == 0 ? h : vmin(hm[q], h);
-    }
-  }
-  f2 zmax[NPR], zl[NPR], se[NPR], z[NPR];
-#pragma unroll
-  for (int q = 0; q < NPR; ++q) {
-    zmax[q] = p.neg_beta * hm[q];
-    zl[q] = zmax[q] * real(1.44269504088896341);
-  }
-#pragma unroll
-  for (int i = 0; i < MO; ++i) {
-#if DTMPC_FAST_F64
-    // one wave-uniform branch per obstacle for all the lane's candidates (smterm)
-    f2 x[NPR], e[NPR];
-    bool need = false;
-#pragma unroll
-    for (int q = 0; q < NPR; ++q) {
-      x[q] = smarg(p, TWO ? hval(i, q) : hi[TWO ? 0 : i][q], zmax[q]);
-      need = need || smneed(x[q]);
-      e[q] = f2(0.0);
-    }
-    if (__builtin_amdgcn_ballot_w64(need))
-#pragma unroll
-      for (int q = 0; q < NPR; ++q) e[q] = smexp(x[q]);
-#pragma unroll
-    for (int q = 0; q < NPR; ++q) se[q] = i == 0 ? e[q] : se[q] + e[q];
-#else
-#pragma unroll
-    for (int q = 0; q < NPR; ++q) {
-      const f2 e = smterm(p, hi[TWO ? 0 : i][q], zmax[q], zl[q]);
-      se[q] = i == 0 ? e : se[q] + e;  // = 0 + e_0 + ...: e_0 >= 0, so 0 + e_0 == e_0 bitwise
-    }
-#endif
-  }
-#pragma unroll
-  for (int q = 0; q < NPR; ++q) {
-    z[q] = p.neg_inv_beta * (zmax[q] + vlog(se[q]));
-    if (Obs<M>::tight) z[q] = z[q] - p.tight;
-  }
-  // relaxed inverse barrier: the reciprocal for every element, the quadratic branch (z < a) once
-  // per step for whichever elements need it
   f2 Bn[NPR];
-  real zmin = z[0].x;
-#pragma unroll
-  for (int q = 0; q < NPR; ++q) {
-    Bn[q] = f2{m_rcp(vmaxnan(z[q].x, p.eps)), m_rcp(vmaxnan(z[q].y, p.eps))};
-    zmin = m_min(zmin, m_min(z[q].x, z[q].y));
-  }
-  if (!(zmin >= p.a)) {
-#pragma unroll
-    for (int q = 0; q < NPR; ++q) {
-      if (!(z[q].x >= p.a)) Bn[q].x = bar_relaxed(p, z[q].x);
-      if (!(z[q].y >= p.a)) Bn[q].y = bar_relaxed(p, z[q].y);
-    }
-  }
+  ls_bar<M, NPR>(p, C.a0, C.a1, Bn);
 #pragma unroll
   for (int q = 0; q < NPR; ++q) {
     if (G0) {  // b' = B(h(x')) (fhat<M, true>)
@@ -1614,6 +1800,72 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
   }
 }
 
+// The same step software-pipelined (f32, gamma = 0, four lanes: one candidate pair per lane, i.e. one dependent
+// chain per step).  At gamma = 0 the controls do not read b (K's b column is zero), so b_k = B(h(x_k)) -- which
+// ls_step evaluates at the end of step k - 1, right after the move that produced x_k -- is evaluated here, in
+// step k, beside the move x_k -> x_{k+1}: two independent chains in one basic block, so the smooth-min's exp /
+// log / rcp latencies fill the move's sin / cos chain.  The out-of-range sin / cos case is redone after them
+// (one uniform branch).  Step 0 takes b_0 from the start state (`first`).  The same operations on the same
+// values as ls_step: bitwise the same candidates.  x_k comes back in xk* for the slot stores (row k = x_k, b_k).
+#ifndef DTMPC_FAST_LS_PIPE
+#define DTMPC_FAST_LS_PIPE 1
+#endif
+#if !DTMPC_FAST_F64 && !defined(DTMPC_OCML_SINCOS)
+template <bool TRACK, int M, int NPR>
+__device__ __forceinline__ void ls_step_pipe(const FP& p, const FCost& c, const StepIn& s, Cand<NPR>& C, f2* u0,
+                                             f2* u1, f2* xk0, f2* xk1, f2* xk2, bool first) {
+  DTMPC_NOCONTRACT
+  static_assert(DTMPC_FAST_KFMA, "the pipelined step is written for the fma feedback");
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    xk0[q] = C.a0[q];
+    xk1[q] = C.a1[q];
+    xk2[q] = C.a2[q];
+    const f2 e0 = C.a0[q] - s.X0, e1 = C.a1[q] - s.X1, e2 = C.a2[q] - s.X2;
+    const f2 du0 = s.kk.x + kdot<true>(s.Ka, e0, e1, e2, e2);
+    const f2 du1 = s.kk.y + kdot<true>(s.Kb, e0, e1, e2, e2);
+    u0[q] = ffma(C.al[q], du0, f2(s.V0));
+    u1[q] = ffma(C.al[q], du1, f2(s.V1));
+  }
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    u0[q] = vclamp(u0[q], p.umin0, p.umax0);
+    u1[q] = vclamp(u1[q], p.umin1, p.umax1);
+  }
+  real m = __builtin_fabsf(xk2[0].x);
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(xk2[q].x), __builtin_fabsf(xk2[q].y)));
+  f2 sn[NPR], cs[NPR];
+  sincos_pairs_fast<NPR>(xk2, sn, cs);
+  auto move = [&]() {
+#pragma unroll
+    for (int q = 0; q < NPR; ++q) {
+      const f2 dv = p.dt * u0[q];
+      C.a0[q] = ffma(dv, cs[q], xk0[q]);
+      C.a1[q] = ffma(dv, sn[q], xk1[q]);
+      C.a2[q] = ffma(f2(p.dt), u1[q], xk2[q]);
+    }
+  };
+  move();
+  f2 Bn[NPR];
+  ls_bar<M, NPR>(p, xk0, xk1, Bn);
+#pragma unroll
+  for (int q = 0; q < NPR; ++q) {
+    const f2 bk = first ? C.ab[q] : Bn[q];
+    C.J[q] = C.J[q] + stage<TRACK, Obs<M>::wrap>(c, xk0[q], xk1[q], xk2[q], bk, u0[q], u1[q], s.r0, s.r1, s.r2,
+                                                  s.q0, s.q1);
+    C.ab[q] = bk;
+  }
+  if (__builtin_expect(!(m <= 65536.0f), 0)) {
+    sincos_pairs<NPR>(xk2, sn, cs);
+    move();
+  }
+}
+#endif
+
+#ifndef DTMPC_FAST_LS_LEAD4
+#define DTMPC_FAST_LS_LEAD4 4  // P = 4: step inputs in a ring of LEAD + 1 buffers refilled LEAD steps ahead (0: two buffers, as P = 1; B = 4,096: 2.13 ms at 0, 2.03 at 3, 2.01 at 4)
+#endif
 // P = 4: the candidate tapes.  Every lane writes the rollouts of its two candidates into their own
 // slots of the solve's tape records (instead of the winner being re-rolled by a commit pass): slot
 // bank * 6 + candidate, in the bank the current tape is not in; the winner's slot then becomes the
@@ -1666,7 +1918,12 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
     else
       C.al[q] = f2{pick3(hc, cf.cal[0], cf.cal[2], cf.cal[4]), pick3(hc, cf.cal[1], cf.cal[3], cf.cal[5])};
   }
-  if (P == 4) {  // the candidates' row 0
+#if !DTMPC_FAST_F64 && !defined(DTMPC_OCML_SINCOS)
+  constexpr bool PIPE = DTMPC_FAST_LS_PIPE && SV::g0 && P == 4 && DTMPC_FAST_LS_LEAD4 > 0;
+#else
+  constexpr bool PIPE = false;
+#endif
+  if (P == 4 && !PIPE) {  // the candidates' row 0 (PIPE: stored by the first step, row k = (x_k, b_k))
     const f4 X0v = f4{x0[0], x0[1], x0[2], x0[3]};
     rst4(S.r, Z.X0, 0, 0, X0v);
     rst4(S.r, Z.X1, 0, 0, X0v);
@@ -1682,9 +1939,6 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   };
   f2 u0[NPR], u1[NPR];
   const int N1 = N - 1;
-#ifndef DTMPC_FAST_LS_LEAD4
-#define DTMPC_FAST_LS_LEAD4 4  // P = 4: step inputs in a ring of LEAD + 1 buffers refilled LEAD steps ahead (0: two buffers, as P = 1; B = 4,096: 2.13 ms at 0, 2.03 at 3, 2.01 at 4)
-#endif
   if (P == 4 && DTMPC_FAST_LS_LEAD4 > 0) {
     constexpr int LEAD = DTMPC_FAST_LS_LEAD4 > 0 ? DTMPC_FAST_LS_LEAD4 : 1, R = LEAD + 1;
     auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
@@ -1696,10 +1950,31 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
       for (int j = 0; j < R; ++j) {
         load_step<TRACK>(Bf[(j + LEAD) % R], S, ix(k + j + LEAD));
         if (k + j >= N) break;
+#if !DTMPC_FAST_F64 && !defined(DTMPC_OCML_SINCOS)
+        if (PIPE) {
+          f2 xk0[NPR], xk1[NPR], xk2[NPR];
+          ls_step_pipe<TRACK, M, NPR>(p, c, Bf[j], C, u0, u1, xk0, xk1, xk2, k + j == 0);
+          rst2(S.r, Z.U0, k + j, 0, f2{u0[0].x, u1[0].x});
+          rst2(S.r, Z.U1, k + j, 0, f2{u0[0].y, u1[0].y});
+          rst4(S.r, Z.X0, k + j, 0, f4{xk0[0].x, xk1[0].x, xk2[0].x, C.ab[0].x});
+          rst4(S.r, Z.X1, k + j, 0, f4{xk0[0].y, xk1[0].y, xk2[0].y, C.ab[0].y});
+          continue;
+        }
+#endif
         ls_step<TRACK, M, NPR, SV::g0>(p, c, Bf[j], C, u0, u1);
         keep(k + j, u0, u1);
       }
     }
+#if !DTMPC_FAST_F64 && !defined(DTMPC_OCML_SINCOS)
+    if (PIPE) {  // b_N of the final states (the terminal cost's) and the slots' row N
+      f2 Bn[NPR];
+      ls_bar<M, NPR>(p, C.a0, C.a1, Bn);
+#pragma unroll
+      for (int q = 0; q < NPR; ++q) C.ab[q] = Bn[q];
+      rst4(S.r, Z.X0, N, 0, f4{C.a0[0].x, C.a1[0].x, C.a2[0].x, C.ab[0].x});
+      rst4(S.r, Z.X1, N, 0, f4{C.a0[0].y, C.a1[0].y, C.a2[0].y, C.ab[0].y});
+    }
+#endif
   } else if (DTMPC_FAST_LS_DEPTH2) {
   // four buffers in rotation, each refilled two steps before use.  RC (gamma = 0, f32): the current tape's
   // states X_k -- and the ancillary's reference states -- are not read but re-rolled from their controls by
@@ -2355,6 +2630,18 @@ __device__ __forceinline__ FP phase_p() {
 #define DTMPC_FAST64_TAB 1
 #endif
 template <int M, int GM>
+constexpr int tab_flag();
+// the exp form of an f64 instantiation: the one-block asm polynomial holds its ten coefficients in VGPRs, which the
+// four-lane kernels and the table-in-kernarg (kLds) ones cannot afford without a private segment (build.py check)
+template <int M, int GM, int P>
+constexpr int xasm_flag() {
+#if DTMPC_FAST_F64
+  return (DTMPC_FAST64_EXP == 3 && P != 4 && tab_flag<M, GM>() == 0) ? kXasm : 0;
+#else
+  return 0;
+#endif
+}
+template <int M, int GM>
 constexpr int tab_flag() {
   return (DTMPC_FAST_F64 && (DTMPC_FAST64_TAB == 2 ||
                              (DTMPC_FAST64_TAB == 1 && (GM == 0 || Obs<M>::n > DTMPC_FAST_PIN64_MAX))))
@@ -2368,7 +2655,7 @@ template <int M, int P, int GM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 tube_fast_kernel(FK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
-  constexpr int ML = M | tab_flag<M, GM>();  // M with the table placement (kLds: LDS, f64 only)
+  constexpr int ML = M | tab_flag<M, GM>() | xasm_flag<M, GM, P>();  // M with the table placement and exp form (f64)
   (void)kk;  // read through kargs()
   __shared__ f4 lds[kBlock / 64 * DTMPC_TUBE_SUMS / 4];  // the workgroup sums at the end
   const int B = kargs()->a.B, Bc = kargs()->a.Bc, i0 = kargs()->a.i0;
@@ -2653,7 +2940,7 @@ ilqr_fast_kernel(IK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
   (void)kk;  // read through ikargs()
   const IArgs& a = ikargs()->a;
-  constexpr int ML = M | tab_flag<M, GM>();
+  constexpr int ML = M | tab_flag<M, GM>() | xasm_flag<M, GM, P>();
   obs_fill<ML>(ikargs()->p);
   const int B = a.B, Bc = a.Bc, i0 = a.i0;
   const int gl = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2779,7 +3066,7 @@ template <int M, int GM>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1)))
 receding_fast_kernel(RK kk) {
   constexpr bool G0 = GM > 0, RG0 = GM > 1;
-  constexpr int ML = M | tab_flag<M, GM>();
+  constexpr int ML = M | tab_flag<M, GM>() | xasm_flag<M, GM, 1>();
   constexpr int MW = ML | kWrap;
   (void)kk;  // read through rkargs()
   obs_fill<ML>(rkargs()->p);
@@ -3114,11 +3401,19 @@ static int fast_g0(const dtmpc_spec* sp) {
 }
 
 #if DTMPC_FAST_F64
-// f64 at four lanes with the general records (gamma != 0): run-to-run different results and non-finite statuses on
-// some trajectories at some obstacle counts, moving with every change of the kernel's code (DESIGN.md section 9,
-// profiles/r05/f64_defect.txt) while the one- and two-lane forms and the compact-record four-lane form are correct
-// at every count -- dtmpc_tube_step runs that family on the generic f64 kernel instead
-bool tube_fast_lanes_ok64(const dtmpc_spec* sp, int lanes) { return !(lanes == 4 && fast_g0(sp) == 0); }
+// f64 general gain records at four lanes.  Round 5 v2 ran them on the generic f64 kernel: the fused form gave
+// run-to-run different results at some obstacle counts and not at others, moving with every change of the kernel.
+// The cause was the store-data hazard of the 128-bit record stores (st128; every f64 record store is 128-bit):
+// since v3 the family runs fused (scripts/diag_records.py: every M = 1-8 at four lanes within 1e-8 of the generic
+// kernel, twice bitwise equal; profiles/r05/diag_records_v3.txt).  DTMPC_FAST64_L4G=0 routes it to the generic
+// kernel again (A/B only).
+bool tube_fast_lanes_ok64(const dtmpc_spec* sp, int lanes) {
+  static const bool generic = [] {
+    const char* e = getenv("DTMPC_FAST64_L4G");
+    return e && e[0] == '0';
+  }();
+  return !(generic && lanes == 4 && fast_g0(sp) == 0);
+}
 #endif
 
 int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, int64_t goff, int64_t step,

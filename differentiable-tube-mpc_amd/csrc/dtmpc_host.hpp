@@ -186,8 +186,8 @@ int launch_tube_fast(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_t B, 
 // the same tube step in f64 (dtmpc_fast64.hip: dtmpc_fast.hip with real = double); its chunk is clamped to
 // tube_fast_chunk_max64 at launch
 bool tube_fast_eligible64(int dtype, const dtmpc_spec* sp, const dtmpc_tube_cfg* cf);
-// false for the f64 instantiations the fused step does not run: the general gain records (gamma != 0, or the
-// DTMPC_FAST_G0=0 switch) at four lanes, which dtmpc_tube_step runs on the generic f64 kernel
+// false for the f64 instantiations the fused step does not run: none since round 5 v3 (DTMPC_FAST64_L4G=0, an A/B
+// switch, routes the general gain records at four lanes to the generic f64 kernel)
 bool tube_fast_lanes_ok64(const dtmpc_spec* sp, int lanes);
 int64_t tube_fast_chunk_max64(int N, int lanes);
 size_t tube_fast_workspace_bytes64(int N, int64_t B, int lanes, int64_t chunk);

@@ -20,13 +20,13 @@ run() {  # name seconds cmd...
   echo "[ab] $name rc=$rc" | tee -a "$OUT/session.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[ab] stop after $name" | tee -a "$OUT/session.log"; exit $rc; fi
 }
-# env: DIAG=0 skips the bitwise check; BENCH_ARGS replaces the headline bench arguments (e.g. the f64 leg);
+# env: DIAG=0 skips the bitwise check (DIAG_CFG: its configuration, e.g. DT=f64,L=1); BENCH_ARGS replaces the headline bench arguments (e.g. the f64 leg);
 # the name "product" is the product library libdtmpc.so
 lib() { if [ "$1" = product ]; then echo "$PWD/$L/libdtmpc.so"; else echo "$PWD/$L/libdtmpc_$1.so"; fi; }
 BARGS=${BENCH_ARGS:---steps 20 --warmup 8 --no-cpu --no-steady --no-extra}
 if [ "${DIAG:-1}" = 1 ]; then
   for v in "$@"; do
-    run diag_$v 180 env DTMPC_LIBRARY=$(lib $v) python scripts/diag_g0.py run "$OUT/$v.npz" "L=1"
+    run diag_$v 180 env DTMPC_LIBRARY=$(lib $v) python scripts/diag_g0.py run "$OUT/$v.npz" "${DIAG_CFG:-L=1}"
   done
   first=$1
   for v in "$@"; do

@@ -74,7 +74,8 @@ def _tube_cfg(st, seed):
 @pytest.mark.parametrize("m", [4, 8])
 def test_tube_step_f64_gamma_vs_oracle(dev, oracle_lib, m, lanes, monkeypatch):
     """Two closed-loop steps of TubeMPC (f64, gamma = 0.3, alpha = 0.05: the fused kernel's general records at
-    one and two lanes; at four lanes dtmpc_tube_step runs this family on the generic f64 kernel)
+    one, two and four lanes -- four lanes ran the generic f64 kernel in round 5 v2 until the store-data hazard was
+    found)
     from the device's own pre-step state, against the oracle's one-step map; status all 0, x / xbar / b, both plans
     and the per-trajectory DOC gradient rows within the f64 band."""
     monkeypatch.setenv("DTMPC_TUBE_LANES", lanes)

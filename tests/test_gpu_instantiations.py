@@ -95,11 +95,10 @@ def test_tube_step_instantiations(dev, tag, m, g0, monkeypatch):
     mode's gamma = 0 -- the kernels any setup with gamma != 0 runs (tests/test_gpu_general_records.py checks them
     against the oracle at gamma = 0.3).  Round 4 had these failing in f64 at M = 4 and 8 (xfail); round 5 found the
     cause in the f64 far-range sin / cos call's out-parameters and the kernels' scratch and
-    every f64 fused kernel now builds without a private segment (build.py check_resources).  f64 general records at
-    four lanes (this batch's own form) run the generic kernel (tube_fast_lanes_ok64), so the f64
-    "0" cases run the fused kernel at two lanes."""
-    if tag == "f64" and g0 == "0":
-        monkeypatch.setenv("DTMPC_TUBE_LANES", "2")
+    every f64 fused kernel now builds without a private segment (build.py check_resources); the last of the family
+    (the four-lane general records, run-to-run different at some M) was the store-data hazard of the 128-bit record
+    stores (csrc/dtmpc_fast.hip st128, build.py store_hazards), so every case here runs this batch's own four-lane
+    form on the fused kernel."""
     from diff_tube_mpc_strict_pt.core import TubeMPC
     from diff_tube_mpc_strict_pt.core.problem import paper_setup_from_config
 

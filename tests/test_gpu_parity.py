@@ -831,14 +831,12 @@ def test_tube_step_fast_gamma0_records(dev, lanes, tag, monkeypatch):
     steps: states, tapes, log rows, partial sums and the shared theta.  DTMPC_FAST_G0=1 is the compact
     records with the general Riccati step; the default at gamma = 0 also drops the barrier state's zero
     column from the recursion (riccati_pk<true>, an FMA rounding of it), which test_tube_step_vs_oracle
-    checks against the oracle builds.  (f64 at four lanes: the general records run the generic f64 kernel,
-    tube_fast_lanes_ok64 -- there the two record forms are two different kernels and not compared bitwise.)"""
+    checks against the oracle builds.  (Round 5 v2 ran the f64 general records at four lanes on the generic
+    kernel and skipped that case; the store-data hazard fix put them back on the fused kernel)"""
     import dataclasses
 
     from diff_tube_mpc_strict_pt.core import TubeMPC
 
-    if tag == "f64" and lanes == "4":
-        pytest.skip("f64 general records at four lanes run the generic kernel (DESIGN.md section 9)")
     monkeypatch.setenv("DTMPC_TUBE_LANES", lanes)
     st = paper_setup()
     assert st.problem.dbas_gamma == 0.0
