@@ -192,13 +192,19 @@ def store_hazards(obj: str) -> list:
     """128-bit (and 96-bit) buffer stores whose data VGPRs a VALU instruction writes within the two wait states
     after the store (the gfx950 store-data hazard the compiler does not pad for buffer stores with an SGPR soffset,
     csrc/dtmpc_fast.hip st128): [(kernel, store line, offending line)] of the code object in a hipcc object."""
-    import re
     import tempfile
 
     with tempfile.TemporaryDirectory() as d:
         co = _code_object(obj, d)
         dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", f"--mcpu={ARCH}", "--no-show-raw-insn",
                               "--no-leading-addr", co], check=True, capture_output=True, text=True).stdout
+    return scan_store_hazards(dis)
+
+
+def scan_store_hazards(dis: str) -> list:
+    """store_hazards on a disassembly text (llvm-objdump -d): [(kernel, store line, offending line)]."""
+    import re
+
     out, kern = [], None
     lines = dis.splitlines()
     for i, line in enumerate(lines):

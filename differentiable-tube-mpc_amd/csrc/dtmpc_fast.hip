@@ -1343,11 +1343,13 @@ __device__ __forceinline__ Lin lin_point(const FP& p, const f4& X) {
 // trajectory, and handed to every lane by DPP broadcasts; the Riccati recursion itself is sequential
 // and runs on every lane (each needs the gains).  Same operations on the same values as P = 1: the
 // gains are bitwise those of the one-lane form.
-#ifndef DTMPC_FAST_BW_OPQ
-#define DTMPC_FAST_BW_OPQ 1
-#endif
+// DTMPC_FAST_BW_BCAST (A/B, default off; DESIGN.md section 3 "Small batches: the four-lane step's latency"): at
+// P > 1 the step inputs handed on from the group's per-lane rows by DPP instead of loaded one step ahead.  Same values
+// (bitwise under -ffp-contract=off), but the compiler contracts the Riccati step differently: B = 4,096 2.04 -> 2.02 ms
+// in this form; the in-step broadcast form (round-5 experiment) ran 1.91 ms but its contraction moved the f32
+// gradient rows below the raw-rate parity gate (0.944 < 0.95), so neither is the product.
 #ifndef DTMPC_FAST_BW_BCAST
-#define DTMPC_FAST_BW_BCAST 1
+#define DTMPC_FAST_BW_BCAST 0
 #endif
 template <bool TRACK, int M, class SV>
 __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, const SV& S, int h) {
@@ -1398,11 +1400,10 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
   real gxn, gyn;
   real dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
   bool ok = finite(RVX(0)) && finite(RVX(1)) && finite(RVX(2)) && finite(RVX(3));
-  // step inputs one step ahead (P > 1 with BW_BCAST: from the group's per-lane rows instead)
-  constexpr bool BCI = P > 1 && DTMPC_FAST_BW_BCAST != 0;
-  f4 nX = BCI ? f4{0.f, 0.f, 0.f, 0.f} : S.x(N - 1), nR = f4{0.f, 0.f, 0.f, 0.f};
-  f2 nV = BCI ? f2{0.f, 0.f} : S.u(N - 1), nQ = f2{0.f, 0.f};
-  if (TRACK && !BCI) {
+  // step inputs one step ahead (P > 1 with BW_BCAST: after the first, from the group's per-lane rows)
+  f4 nX = S.x(N - 1), nR = f4{0.f, 0.f, 0.f, 0.f};
+  f2 nV = S.u(N - 1), nQ = f2{0.f, 0.f};
+  if (TRACK) {
     nR = S.xr(N - 1);
     nQ = S.ur(N - 1);
   }
@@ -1531,23 +1532,22 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
       for (int j = 0; j < P; ++j) {
         const int k = kt - j;
         if (k < 0) break;
-        f4 X = nX, Rr = nR;
-        f2 V = nV, Q = nQ;
+        const f4 X = nX, Rr = nR;
+        const f2 V = nV, Q = nQ;
         if (BC) {
-          // each broadcast value made opaque, as a loaded value is: the step's arithmetic then compiles as in the
-          // load form (the same FMA contraction of the Riccati step, so the same gains bit for bit)
-          auto bq = [&](real v) {
-            real w = gbcast<P>(v, j);
-#if DTMPC_FAST_BW_OPQ
-            __asm__("" : "+v"(w));
-#endif
-            return w;
-          };
-          X = f4{bq(PXc.x), bq(PXc.y), bq(PXc.z), bq(PXc.w)};
-          V = f2{bq(PVc.x), bq(PVc.y)};
-          if (TRACK) {
-            Rr = f4{bq(PRc.x), bq(PRc.y), bq(PRc.z), 0.f};
-            Q = f2{bq(PQc.x), bq(PQc.y)};
+          // the inputs of step k - 1, handed on to the next step as next_inputs hands on its loads (the step
+          // itself then reads loop-carried values in both forms): row k - 1 from lane j + 1 of this group, or from
+          // lane 0 of the next group's rows
+          if (k > 0) {
+            const int jn = j + 1 < P ? j + 1 : 0;
+            const f4 XS = j + 1 < P ? PXc : PX, RS = j + 1 < P ? PRc : PR;
+            const f2 VS = j + 1 < P ? PVc : PV, QS = j + 1 < P ? PQc : PQ;
+            nX = f4{gbcast<P>(XS.x, jn), gbcast<P>(XS.y, jn), gbcast<P>(XS.z, jn), gbcast<P>(XS.w, jn)};
+            nV = f2{gbcast<P>(VS.x, jn), gbcast<P>(VS.y, jn)};
+            if (TRACK) {
+              nR = f4{gbcast<P>(RS.x, jn), gbcast<P>(RS.y, jn), gbcast<P>(RS.z, jn), 0.f};
+              nQ = f2{gbcast<P>(QS.x, jn), gbcast<P>(QS.y, jn)};
+            }
           }
         } else {
           next_inputs(k);
@@ -1808,7 +1808,7 @@ __device__ __forceinline__ void ls_step(const FP& p, const FCost& c, const StepI
 // (one uniform branch).  Step 0 takes b_0 from the start state (`first`).  The same operations on the same
 // values as ls_step: bitwise the same candidates.  x_k comes back in xk* for the slot stores (row k = x_k, b_k).
 #ifndef DTMPC_FAST_LS_PIPE
-#define DTMPC_FAST_LS_PIPE 1
+#define DTMPC_FAST_LS_PIPE 0  // A/B: bitwise the same tapes, same time (B = 4,096: 1.91 ms both ways), so off
 #endif
 #if !DTMPC_FAST_F64 && !defined(DTMPC_OCML_SINCOS)
 template <bool TRACK, int M, int NPR>
