@@ -1,6 +1,6 @@
 """Diagnostic (GPU): where do configurations of the fast tube step differ?  usage:
   python scripts/diag_g0.py run OUT.npz "G0=1,L=1"     one and two closed-loop steps of a B = 700 batch (f32;
-                                                      "DT=f64" for f64) under DTMPC_FAST_G0 / DTMPC_TUBE_LANES /
+                                                      "DT=f64" for f64; "SEED=5" the start states' seed) under DTMPC_FAST_G0 / DTMPC_TUBE_LANES /
                                                       DTMPC_FAST64 ("F64=0": the generic f64 kernel) and the
                                                       library named by DTMPC_LIBRARY, saved
   python scripts/diag_g0.py cmp BASE.npz A.npz ...    per state array: bitwise equal or the max difference"""
@@ -20,10 +20,14 @@ def run(out, cfg):
     import torch
 
     dt_name = "f32"
+    seed = 6
     for kv in cfg.split(","):
         k, v = kv.split("=")
         if k == "DT":
             dt_name = v
+            continue
+        if k == "SEED":
+            seed = int(v)
             continue
         os.environ[{"G0": "DTMPC_FAST_G0", "L": "DTMPC_TUBE_LANES", "F64": "DTMPC_FAST64"}[k]] = v
     from _common import paper_setup
@@ -33,7 +37,7 @@ def run(out, cfg):
     st = dataclasses.replace(st, ilqr_nom=dataclasses.replace(st.ilqr_nom, tol=-1.0),
                              ilqr_aux=dataclasses.replace(st.ilqr_aux, tol=-1.0))
     B = 700
-    rng = np.random.default_rng(6)
+    rng = np.random.default_rng(seed)
     tdt = torch.float32 if dt_name == "f32" else torch.float64
     x = torch.tensor(np.stack([rng.uniform(0, 1, B), rng.uniform(0, 1, B), rng.uniform(0, np.pi / 2, B)], 1),
                      dtype=tdt)
