@@ -2632,11 +2632,15 @@ __device__ __forceinline__ FP phase_p() {
 template <int M, int GM>
 constexpr int tab_flag();
 // the exp form of an f64 instantiation: the one-block asm polynomial holds its ten coefficients in VGPRs, which the
-// four-lane kernels and the table-in-kernarg (kLds) ones cannot afford without a private segment (build.py check)
+// four-lane kernels and the table-in-kernarg (kLds) ones cannot afford without a private segment (build.py check).
+// One lane only: at two lanes the asm form's closed loop depended on what earlier runs left in the (uninitialised)
+// workspace on one trajectory of 700 (scripts/diag_reuse.py with the workspace pre-filled; the compiled-fma form,
+// and the asm form without the store guard, were clean) -- not root-caused, so that form stays where the same check
+// is clean (tests/test_gpu_reuse.py)
 template <int M, int GM, int P>
 constexpr int xasm_flag() {
 #if DTMPC_FAST_F64
-  return (DTMPC_FAST64_EXP == 3 && P != 4 && tab_flag<M, GM>() == 0) ? kXasm : 0;
+  return (DTMPC_FAST64_EXP == 3 && P == 1 && tab_flag<M, GM>() == 0) ? kXasm : 0;
 #else
   return 0;
 #endif
