@@ -412,6 +412,8 @@ def main() -> None:
     ap.add_argument("--no-steady", action="store_true", help="skip the free-running (warm-started) loop field")
     ap.add_argument("--no-overlap", action="store_true",
                     help="N > 1: all-reduce theta in line instead of beside the next step's nominal solve (TubeMPC overlap)")
+    ap.add_argument("--no-weak-leg", action="store_true",
+                    help="N > 1: skip the weak-scaling leg (65,536 trajectories per GPU) beside the strong-scaling line")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary legs (f64 tube step, config-2 nominal DDP at B = 4096)")
     ap.add_argument("--workload", default="tube", choices=["tube", "nominal-ddp", "receding"],
@@ -506,9 +508,12 @@ def main() -> None:
     if args.dry_run:
         ev = kev = None
     else:
-        # HIP events on the launch stream: whole step, and the fused tube_step kernel alone
+        # HIP events on the launch stream: whole step, and the fused tube_step kernel alone -- in overlap mode around
+        # each of its two launches (phase 1: nominal, phase 2: the rest), so the kernel time excludes the launch
+        # stream's wait for the previous step's theta update (end of phase 1 -> start of phase 2), reported beside it
+        nkev = 4 if mpc.overlap else 2
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-        kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        kev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(nkev)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     for s in range(args.steps):
         if ev is not None:
@@ -519,9 +524,14 @@ def main() -> None:
             step()
     barrier()
     wall = time.perf_counter() - t0
+    wait_ms = 0.0
     if ev is not None:
         step_ms = [e0.elapsed_time(e1) for e0, e1 in ev]
-        kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in kev]))
+        if mpc.overlap:
+            kern_ms = float(np.mean([k[0].elapsed_time(k[1]) + k[2].elapsed_time(k[3]) for k in kev]))
+            wait_ms = float(np.mean([k[1].elapsed_time(k[2]) for k in kev]))
+        else:
+            kern_ms = float(np.mean([k[0].elapsed_time(k[1]) for k in kev]))
         # f32 can overflow on trajectories driven deep into an obstacle's relaxed barrier, exactly where
         # the reference raises FloatingPointError in f32; such trajectories are flagged and counted
         flagged_local = int((mpc.status != 0).sum())
@@ -529,10 +539,22 @@ def main() -> None:
         step_ms, kern_ms, flagged_local = [1e3 * wall / max(args.steps, 1)], 1e3 * wall / max(args.steps, 1), 0
     red = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
     cnt = torch.tensor([flagged_local], dtype=torch.int64, device=dev)
+    # every rank's own figures (the first multi-GPU run must explain itself): its shard, kernel time,
+    # the launch stream's wait for the theta update, the whole-step wall time and whether the overlap path ran
+    mine = torch.tensor([rank, hi - lo, kern_ms, wait_ms, 1e3 * wall / max(args.steps, 1),
+                         float(bool(mpc is not None and mpc.overlap)), float(mpc.lanes if mpc is not None else 0)],
+                        dtype=torch.float64, device=dev)
+    gathered = [torch.zeros_like(mine) for _ in range(world)]
     if world > 1:
         dist.all_reduce(red, op=dist.ReduceOp.MAX)  # the slowest rank sets the step time
         dist.all_reduce(cnt)
+        dist.all_gather(gathered, mine)
+    else:
+        gathered = [mine]
     wall, kern_ms_max = float(red[0]), float(red[1])
+    per_rank = [{"rank": int(g[0]), "batch": int(g[1]), "kernel_ms": float(g[2]), "theta_wait_ms": float(g[3]),
+                 "wall_ms_per_step": float(g[4]), "overlap": bool(g[5]), "lanes": int(g[6])}
+                for g in (t.cpu() for t in gathered)]
 
     # second field: the free-running Algorithm-2 loop -- one episode start, then warm-started steps t >= 1
     # (shifted warm starts, advanced plant, theta updated by the batch-mean gradient under the f32 health
@@ -557,6 +579,42 @@ def main() -> None:
                   "theta": [float(v) for v in th], "theta_finite": bool(torch.isfinite(th).all()),
                   "healthy_fraction_last_step": mpc.healthy_count / Bg,
                   "grad_bound": float(mpc.cfg.grad_bound)}
+
+    # N > 1, strong scaling (the default): the same step with BASELINE config 5's 65,536 trajectories PER GPU beside the
+    # strong-scaling line (the per-GPU shard of the fixed global batch shrinks to 8,192 at N = 8, into the small-batch
+    # regime) -- value = N x 65,536 x 31 / the slowest rank's step time
+    weak = None
+    if world > 1 and not args.weak and not args.no_weak_leg:
+        Bw = 65536
+        lo_w, hi_w = shard_range(Bw * world, rank, world)
+        if args.dry_run:
+            def wstep():
+                time.sleep(0.002)
+            ov = False
+        else:
+            del mpc
+            torch.cuda.empty_cache()
+            mpc = TubeMPC(setup, batch=hi_w - lo_w, device=dev, dtype=dtype, disturbance="philox", seed=0,
+                          global_offset=lo_w, global_batch=Bw * world, process_group=None,
+                          overlap=False if args.no_overlap else None)
+            xw = initial_states(lo_w, hi_w, dev, dtype)
+            ov = mpc.overlap
+
+            def wstep():
+                mpc.reset(xw)
+                mpc.step()
+        for _ in range(max(nwarm // 2, args.warmup)):
+            wstep()
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            wstep()
+        barrier()
+        tw = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+        tw = float(tw) / args.steps
+        weak = {"scaling": "weak", "batch_per_gpu": hi_w - lo_w, "global_batch": Bw * world, "ms_per_step": 1e3 * tw,
+                "value": Bw * world * ITERS_PER_STEP / tw, "overlap": ov}
 
     ms_per_step = 1e3 * wall / args.steps
     value = Bg * ITERS_PER_STEP / (wall / args.steps)
@@ -587,6 +645,14 @@ def main() -> None:
         "overlap": bool(mpc.overlap) if mpc is not None else False,
         "kernel_ms": kern_ms,
         "kernel_ms_max_over_ranks": kern_ms_max,
+        # per rank: shard, fused-kernel time (overlap: the two launches' sum), the launch stream's wait for the
+        # previous step's theta all-reduce + update (0 without overlap), wall time per step, overlap path, lanes.
+        # RCCL unmeasured until the driver's multi-GPU run (one-GPU boxes only in this build's budget).
+        "ranks": per_rank,
+        "comm": {"backend": (dist.get_backend() if dist.is_initialized() else None),
+                 "collective": "all_reduce(SUM) of 8 floats per step" if world > 1 else None,
+                 "overlap": bool(mpc.overlap) if mpc is not None else False,
+                 "theta_wait_ms_max_over_ranks": max(r["theta_wait_ms"] for r in per_rank)},
         "flagged_trajectories": int(cnt[0]),
         "event_ms_per_step_median": float(np.median(step_ms)),
         "warmup_run": nwarm,
@@ -595,6 +661,7 @@ def main() -> None:
                                 batch=hi - lo),
     }
     out["steady_state"] = steady
+    out["weak_scaling"] = weak
     if world == 1 and not args.dry_run and not args.no_extra:
         # secondary legs: the reference's configured precision (configs/dubins.yaml:8,
         # f64) on the same tube step, and BASELINE config 2 (batched nominal DDP, B = 4,096) in f32 / f64

@@ -304,13 +304,31 @@ __device__ __forceinline__ void st128(D d, Rsrc r, unsigned voff, unsigned soff)
 #if DTMPC_FAST_F64
 // f64: a 4-value row is 32 bytes (two 16-byte accesses), a 2-value row 16 bytes (one)
 typedef double d2v __attribute__((ext_vector_type(2)));
+#ifdef DTMPC_DIAG_STALE
+// diagnostics builds (scripts/diag_stale.py): a workspace pre-filled with 0xff bytes holds the all-ones pattern, which
+// no arithmetic produces (a computed NaN is 0x7ff8...): a record load that returns it read a slot this run never wrote
+__device__ __noinline__ void stale_hit(unsigned base, unsigned so, unsigned vo, int which) {
+  printf("STALE blk=%d thr=%d base=%u soff=%u voff=%u part=%d\n", (int)blockIdx.x, (int)threadIdx.x, base, so, vo, which);
+}
+__device__ __forceinline__ void stale_chk(d2v v, const RA& a, int k, unsigned off, int which) {
+  const unsigned long long ones = ~0ull;
+  if (__builtin_bit_cast(unsigned long long, v.x) == ones || __builtin_bit_cast(unsigned long long, v.y) == ones)
+    stale_hit(a.base, a.so(k), a.lo + off, which);
+}
+#else
+__device__ __forceinline__ void stale_chk(d2v, const RA&, int, unsigned, int) {}
+#endif
 __device__ __forceinline__ f4 rld4(Rsrc r, const RA& a, int k, unsigned off) {
   const d2v lo = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off, a.so(k), 0));
   const d2v hi = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off + 16u, a.so(k), 0));
+  stale_chk(lo, a, k, off, 0);
+  stale_chk(hi, a, k, off, 1);
   return f4{lo.x, lo.y, hi.x, hi.y};
 }
 __device__ __forceinline__ f2 rld2(Rsrc r, const RA& a, int k, unsigned off) {
-  return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off, a.so(k), 0));
+  const d2v v = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(r, a.lo + off, a.so(k), 0));
+  stale_chk(v, a, k, off, 2);
+  return __builtin_bit_cast(f2, v);
 }
 __device__ __forceinline__ void rst4(Rsrc r, const RA& a, int k, unsigned off, f4 v) {
   st128(d2v{v.x, v.y}, r, a.lo + off, a.so(k));
@@ -1400,10 +1418,12 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
   real gxn, gyn;
   real dBn = dbarrier(p, h_grad<M>(p, xn0, xn1, gxn, gyn));
   bool ok = finite(RVX(0)) && finite(RVX(1)) && finite(RVX(2)) && finite(RVX(3));
-  // step inputs one step ahead (P > 1 with BW_BCAST: after the first, from the group's per-lane rows)
-  f4 nX = S.x(N - 1), nR = f4{0.f, 0.f, 0.f, 0.f};
-  f2 nV = S.u(N - 1), nQ = f2{0.f, 0.f};
-  if (TRACK) {
+  // step inputs one step ahead (P > 1 with BW_BCAST 1: after the first, from the group's per-lane rows; 2: none, every
+  // step takes its inputs from the group's rows by broadcast)
+  constexpr bool BCI = P > 1 && DTMPC_FAST_BW_BCAST == 2;
+  f4 nX = BCI ? f4{0.f, 0.f, 0.f, 0.f} : S.x(N - 1), nR = f4{0.f, 0.f, 0.f, 0.f};
+  f2 nV = BCI ? f2{0.f, 0.f} : S.u(N - 1), nQ = f2{0.f, 0.f};
+  if (TRACK && !BCI) {
     nR = S.xr(N - 1);
     nQ = S.ur(N - 1);
   }
@@ -1532,9 +1552,17 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
       for (int j = 0; j < P; ++j) {
         const int k = kt - j;
         if (k < 0) break;
-        const f4 X = nX, Rr = nR;
-        const f2 V = nV, Q = nQ;
-        if (BC) {
+        f4 X = nX, Rr = nR;
+        f2 V = nV, Q = nQ;
+        if (BCI) {
+          // BW_BCAST 2 (in-step): step k's inputs from lane j of this group (row kt - j = k), broadcast in the step
+          X = f4{gbcast<P>(PXc.x, j), gbcast<P>(PXc.y, j), gbcast<P>(PXc.z, j), gbcast<P>(PXc.w, j)};
+          V = f2{gbcast<P>(PVc.x, j), gbcast<P>(PVc.y, j)};
+          if (TRACK) {
+            Rr = f4{gbcast<P>(PRc.x, j), gbcast<P>(PRc.y, j), gbcast<P>(PRc.z, j), 0.f};
+            Q = f2{gbcast<P>(PQc.x, j), gbcast<P>(PQc.y, j)};
+          }
+        } else if (BC) {
           // the inputs of step k - 1, handed on to the next step as next_inputs hands on its loads (the step
           // itself then reads loop-carried values in both forms): row k - 1 from lane j + 1 of this group, or from
           // lane 0 of the next group's rows
@@ -1586,6 +1614,11 @@ __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, 
 // controls at gamma = 0 in f32 instead of reading them: -16 (nominal) / -32 (ancillary) B of reads per step,
 // bitwise the same tapes; same-box A/B (profiles/r04/ab_recompute.txt) time +-0, HBM traffic -15 %
 #define DTMPC_FAST_LS_RECOMP 1
+#endif
+#ifndef DTMPC_FAST64_RECOMP
+// f64: the same re-roll in the f64 line search and commit (the f64 step reads 43.1 GB per launch
+// against 35.96 GB algorithmic because its passes read the tape states the f32 kernel re-rolls)
+#define DTMPC_FAST64_RECOMP 0
 #endif
 template <int NPR>
 struct Cand {
@@ -1975,14 +2008,13 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
       rst4(S.r, Z.X1, N, 0, f4{C.a0[0].y, C.a1[0].y, C.a2[0].y, C.ab[0].y});
     }
 #endif
-  } else if (DTMPC_FAST_LS_DEPTH2) {
-  // four buffers in rotation, each refilled two steps before use.  RC (gamma = 0, f32): the current tape's
-  // states X_k -- and the ancillary's reference states -- are not read but re-rolled from their controls by
-  // the same Dubins arithmetic that produced them (init_tape / commit / the nominal's solve: rollout(x0, U)),
-  // so they are bit for bit the stored rows; their b is never needed (K's b column is zero at gamma = 0)
-  constexpr bool RC = DTMPC_FAST_LS_RECOMP && SV::g0 && !DTMPC_FAST_F64;
+  } else {
+  // RC (gamma = 0; f32, and f64 with DTMPC_FAST64_RECOMP): the current tape's states X_k -- and the ancillary's
+  // reference states -- are not read but re-rolled from their controls by the same Dubins arithmetic that produced
+  // them (init_tape / commit / the nominal's solve: rollout(x0, U)), so they are bit for bit the stored rows; their
+  // b is never needed (K's b column is zero at gamma = 0)
+  constexpr bool RC = DTMPC_FAST_LS_RECOMP && SV::g0 && (!DTMPC_FAST_F64 || DTMPC_FAST64_RECOMP);
   constexpr bool RCR = RC && SV::rroll;  // the references re-rolled too (only when they are a device rollout)
-  auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
   real o0 = x0[0], o1 = x0[1], o2 = x0[2], q0 = 0.f, q1 = 0.f, q2 = 0.f;
   if (RCR && TRACK) {
     const f4 R0 = S.xr(0);
@@ -2004,6 +2036,9 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
       }
     }
   };
+  if (DTMPC_FAST_LS_DEPTH2) {
+  // four buffers in rotation, each refilled two steps before use
+  auto ix = [&](int j) { return uidx(j < N1 ? j : N1); };
   StepIn A, Bs, Cs, Ds;
   load_step<TRACK, !RC, SV, !RCR>(A, S, 0);
   load_step<TRACK, !RC, SV, !RCR>(Bs, S, ix(1));
@@ -2032,17 +2067,20 @@ __device__ __forceinline__ int line_search(const FP& p, const FCost& c, const FI
   // two step buffers in turn (no copies), each refilled two steps ahead; the refill index is clamped
   // (a redundant load of the last row instead of a branch)
   StepIn A, Bs;
-  load_step<TRACK>(A, S, 0);
-  load_step<TRACK>(Bs, S, N1 < 1 ? N1 : 1);
+  load_step<TRACK, !RC, SV, !RCR>(A, S, 0);
+  load_step<TRACK, !RC, SV, !RCR>(Bs, S, N1 < 1 ? N1 : 1);
   for (int k = 0; k < N; k += 2) {
+    roll(A);
     ls_step<TRACK, M, NPR, SV::g0>(p, c, A, C, u0, u1);
     keep(k, u0, u1);
-    load_step<TRACK>(A, S, uidx(k + 2 < N1 ? k + 2 : N1));
+    load_step<TRACK, !RC, SV, !RCR>(A, S, uidx(k + 2 < N1 ? k + 2 : N1));
     if (k + 1 < N) {
+      roll(Bs);
       ls_step<TRACK, M, NPR, SV::g0>(p, c, Bs, C, u0, u1);
       keep(k + 1, u0, u1);
-      load_step<TRACK>(Bs, S, uidx(k + 3 < N1 ? k + 3 : N1));
+      load_step<TRACK, !RC, SV, !RCR>(Bs, S, uidx(k + 3 < N1 ? k + 3 : N1));
     }
+  }
   }
   }
   real r0 = 0.f, r1 = 0.f, r2 = 0.f;
@@ -2162,7 +2200,7 @@ __device__ __forceinline__ void commit(const FP& p, real al, const real* x0, rea
   // re-rolling the old controls by its Dubins part reproduces the old x, y, theta bit for bit (b is never
   // used: K's b column is zero) and saves 16 B per step of HBM reads.  (With gamma != 0 the re-roll would need
   // the barrier too, measured slower in round 2; f64 is instruction-bound: both read the old states.)
-  constexpr bool CMR = DTMPC_FAST_CM_RECOMP && SV::g0 && !DTMPC_FAST_F64;
+  constexpr bool CMR = DTMPC_FAST_CM_RECOMP && SV::g0 && (!DTMPC_FAST_F64 || DTMPC_FAST64_RECOMP);
   real o0 = s0, o1 = s1, o2 = s2;
   constexpr bool LX = !CMR;
   Solve<false, SV::g0, SV::ric0, SV::lanes> T0;  // no references needed
@@ -2624,8 +2662,9 @@ __device__ __forceinline__ FP phase_p() {
 // private segment (build.py check_resources: the f64 defects of rounds 3-4 all came from f64 kernels that kept
 // values in scratch inside per-lane divergent loops).  The table pinned in VGPRs (pin_p) fits
 // beside the compact gamma = 0 records up to DTMPC_FAST_PIN64_MAX obstacles; the general records (GM = 0, and the
-// general path's solves, which hold both record forms) and larger tables read it from LDS at each use (kLds).
-// DTMPC_FAST64_TAB: 1 that rule (default), 2 LDS in every f64 kernel, 0 never LDS (the round-4 forms, A/B).
+// general path's solves, which hold both record forms) and larger tables read it again at each use (kLds) -- by a
+// scalar load of the kernarg segment's copy (DTMPC_FAST64_TABSRC = 1, the default; 0 is the LDS copy, A/B only).
+// DTMPC_FAST64_TAB: 1 that rule (default), 2 kLds in every f64 kernel, 0 never kLds (the round-4 forms, A/B).
 #ifndef DTMPC_FAST64_TAB
 #define DTMPC_FAST64_TAB 1
 #endif
@@ -2637,10 +2676,13 @@ constexpr int tab_flag();
 // workspace on one trajectory of 700 (scripts/diag_reuse.py with the workspace pre-filled; the compiled-fma form,
 // and the asm form without the store guard, were clean) -- not root-caused, so that form stays where the same check
 // is clean (tests/test_gpu_reuse.py)
+#ifndef DTMPC_FAST64_XASM_MAXP
+#define DTMPC_FAST64_XASM_MAXP 1
+#endif
 template <int M, int GM, int P>
 constexpr int xasm_flag() {
 #if DTMPC_FAST_F64
-  return (DTMPC_FAST64_EXP == 3 && P == 1 && tab_flag<M, GM>() == 0) ? kXasm : 0;
+  return (DTMPC_FAST64_EXP == 3 && P <= DTMPC_FAST64_XASM_MAXP && tab_flag<M, GM>() == 0) ? kXasm : 0;
 #else
   return 0;
 #endif
@@ -2897,6 +2939,49 @@ __global__ void __launch_bounds__(kBlock) record_stream_kernel(const real* src, 
   for (int k = 0; k <= N; ++k) {
     rst4(rd, XA, k, 0, rld4(rs, XA, k, 0));
     if (k < N) rst2(rd, UA, k, 0, rld2(rs, UA, k, 0));
+  }
+}
+
+// The headline kernel's record stream on its own (what HBM delivers to THIS access pattern at THIS
+// occupancy, not to a float4 copy at full occupancy): one lane per trajectory, per pass and step one 16-B X row and
+// one 8-B U row of the current bank and one 32-B gain record read, the other bank's X and U rows written -- 56 B
+// read : 24 B written (70 % read, the step's measured mix is 69 %), every access a buffer access with the row base
+// in soffset and the lane's record in voffset, as the tube kernel addresses them; loads issued D steps ahead (a ring
+// of D + 1 rows).  Records: bank 0 X [N][B][4] U [N][B][2], bank 1 the same, K [N][B][8] (80 B per trajectory-step).
+template <int D>
+__global__ void __launch_bounds__(kBlock) stream_probe_kernel(real* base, int B, int N, int passes, unsigned bytes) {
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= B) return;
+  const Rsrc r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)bytes, 0x00020000);
+  const unsigned cb = (unsigned)B, X = cb * N * 16u, U = cb * N * 8u;
+  const RA XA[2] = {{0, cb * 16u, (unsigned)t * 16u}, {X + U, cb * 16u, (unsigned)t * 16u}};
+  const RA UA[2] = {{X, cb * 8u, (unsigned)t * 8u}, {2 * X + U, cb * 8u, (unsigned)t * 8u}};
+  const RA KA{2 * (X + U), cb * 32u, (unsigned)t * 32u};
+  for (int p = 0; p < passes; ++p) {
+    const int s = p & 1;
+    f4 xq[D + 1], ka[D + 1], kb[D + 1];
+    f2 uq[D + 1];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      xq[j] = rld4(r, XA[s], j, 0);
+      uq[j] = rld2(r, UA[s], j, 0);
+      ka[j] = rld4(r, KA, j, 0);
+      kb[j] = rld4(r, KA, j, 16);
+    }
+    for (int k = 0; k < N; k += D + 1) {
+#pragma unroll
+      for (int j = 0; j <= D; ++j) {
+        const int kk = k + j, kn = uidx(kk + D < N ? kk + D : N - 1);
+        const int q = (j + D) % (D + 1);
+        xq[q] = rld4(r, XA[s], kn, 0);
+        uq[q] = rld2(r, UA[s], kn, 0);
+        ka[q] = rld4(r, KA, kn, 0);
+        kb[q] = rld4(r, KA, kn, 16);
+        if (kk >= N) break;
+        rst4(r, XA[1 - s], kk, 0, xq[j] + ka[j]);
+        rst2(r, UA[1 - s], kk, 0, uq[j] + f2{kb[j].x, kb[j].y});
+      }
+    }
   }
 }
 #endif
@@ -3800,6 +3885,22 @@ int dtmpc_diag_record_stream(int64_t B, int32_t N, const void* src, void* dst, v
   hipLaunchKernelGGL(dtmpc::FK_NS::record_stream_kernel, dtmpc::grid_for(B), dim3(dtmpc::kBlock), 0, (hipStream_t)stream,
                      (const float*)src, (float*)dst, (int)B, (int)N, (unsigned)bytes);
   return dtmpc::check_launch("record_stream_kernel");
+}
+// diagnostics: stream_probe_kernel<depth> (depth 0, 1, 2 or 4) over one buffer of B x N x 80 bytes (< 2^31)
+int dtmpc_diag_stream_probe(int64_t B, int32_t N, int32_t passes, int32_t depth, void* buf, void* stream) {
+  const int64_t bytes = B * (int64_t)N * 80;
+  if (B < 1 || N < 8 || passes < 1 || bytes >= 0x7fffffff || !buf) return dtmpc::set_err(DTMPC_ERR_BAD_ARG, "bad sizes");
+  const dim3 g = dtmpc::grid_for(B), b = dim3(dtmpc::kBlock);
+  hipStream_t st = (hipStream_t)stream;
+  float* p = (float*)buf;
+  switch (depth) {
+    case 0: hipLaunchKernelGGL(dtmpc::FK_NS::stream_probe_kernel<0>, g, b, 0, st, p, (int)B, (int)N, (int)passes, (unsigned)bytes); break;
+    case 1: hipLaunchKernelGGL(dtmpc::FK_NS::stream_probe_kernel<1>, g, b, 0, st, p, (int)B, (int)N, (int)passes, (unsigned)bytes); break;
+    case 2: hipLaunchKernelGGL(dtmpc::FK_NS::stream_probe_kernel<2>, g, b, 0, st, p, (int)B, (int)N, (int)passes, (unsigned)bytes); break;
+    case 4: hipLaunchKernelGGL(dtmpc::FK_NS::stream_probe_kernel<4>, g, b, 0, st, p, (int)B, (int)N, (int)passes, (unsigned)bytes); break;
+    default: return dtmpc::set_err(DTMPC_ERR_BAD_ARG, "depth must be 0, 1, 2 or 4");
+  }
+  return dtmpc::check_launch("stream_probe_kernel");
 }
 }
 

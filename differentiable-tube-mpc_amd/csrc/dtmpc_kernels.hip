@@ -817,8 +817,9 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
   if (cfg->disturbance == 0 && !w) return set_err(DTMPC_ERR_BAD_ARG, "injected disturbance w is NULL");
   if (cfg->disturbance != 0 && cfg->disturbance != 1) return set_err(DTMPC_ERR_BAD_ARG, "bad disturbance mode");
   if (S->phase < 0 || S->phase > 2) return set_err(DTMPC_ERR_BAD_ARG, "state->phase must be 0, 1 or 2");
-  if (S->phase != 0 && !dtmpc_tube_split_supported(dtype, spec, cfg, S->lanes))
-    return set_err(DTMPC_ERR_BAD_ARG, "a split step (state->phase 1 / 2) needs the fused kernel");
+  if (S->phase != 0 && !dtmpc_tube_split_ok(dtype, spec, cfg, B, S->lanes, S->chunk))
+    return set_err(DTMPC_ERR_BAD_ARG, "a split step (state->phase 1 / 2) needs the fused kernel and B within one launch "
+                                      "chunk of the precision (dtmpc_tube_split_ok)");
   hipStream_t st = (hipStream_t)stream;
   if (tube_fast_eligible(dtype, spec, cfg)) return launch_tube_fast(spec, cfg, B, global_offset, step, S, w, st);
   if (tube_fast_eligible64(dtype, spec, cfg) && tube_fast_lanes_ok64(spec, S->lanes))
@@ -832,6 +833,23 @@ int32_t dtmpc_tube_split_supported(int dtype, const dtmpc_spec* spec, const dtmp
   if (!spec || !cfg) return 0;
   return (tube_fast_eligible(dtype, spec, cfg) ||
           (tube_fast_eligible64(dtype, spec, cfg) && tube_fast_lanes_ok64(spec, lanes))) ? 1 : 0;
+}
+
+// ABI 7: the split needs the nominal records of the WHOLE batch between the two launches, i.e. one launch
+// chunk -- the precision's own chunk: f64 records are twice as large, so launch_tube_fast64 clamps the state's chunk to
+// tube_fast_chunk_max64, about half the f32 one
+int32_t dtmpc_tube_split_ok(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B, int32_t lanes,
+                            int64_t chunk) {
+  if (!dtmpc_tube_split_supported(dtype, spec, cfg, lanes) || B < 1 || chunk < 1) return 0;
+  int64_t c = chunk;
+  if (dtype == DTMPC_F64) {
+    const int64_t c64 = tube_fast_chunk_max64(spec->horizon, lanes);
+    c = c < c64 ? c : c64;
+  } else {
+    const int64_t c32 = tube_fast_chunk_max(spec->horizon, lanes);
+    c = c < c32 ? c : c32;
+  }
+  return B <= c ? 1 : 0;
 }
 
 int dtmpc_partials_reduce(int dtype, int64_t n, const void* partials, void* sums, void* stream) {

@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_OBS = 16
 MAX_ALPHAS = 8
 MAX_HORIZON = 512
@@ -208,6 +208,7 @@ PROTOTYPES = {
     "dtmpc_tube_lanes": (I32, [I64]),
     "dtmpc_tube_lanes_dtype": (I32, [I64, C.c_int]),
     "dtmpc_tube_split_supported": (I32, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcTubeCfg), I32]),
+    "dtmpc_tube_split_ok": (I32, [C.c_int, C.POINTER(DtmpcSpec), C.POINTER(DtmpcTubeCfg), C.c_int64, I32, C.c_int64]),
     "dtmpc_tube_partials_count": (I64, [I64, I32]),
     "dtmpc_tube_step": (
         C.c_int,

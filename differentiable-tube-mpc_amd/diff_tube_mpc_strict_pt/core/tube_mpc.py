@@ -162,10 +162,13 @@ class TubeMPC:
         self.work = torch.empty(wbytes, dtype=torch.uint8, device=self.device)
         self.n_partials = int(self.lib.dtmpc_tube_partials_count(B, self.lanes))
         self.partials = torch.zeros(self.n_partials, _abi.TUBE_SUMS, **kw)
-        self.sums = torch.zeros(_abi.TUBE_SUMS, **kw)
+        # theta, vel and sums are written by the theta update, which overlap mode runs on a side stream after step()
+        # returns: the public names are properties that join() first, the buffers live here
+        self._sums = torch.zeros(_abi.TUBE_SUMS, **kw)
         self._theta0 = torch.tensor(setup.theta0, **kw)
-        self.theta = self._theta0.clone()
-        self.vel = torch.zeros(6, **kw)
+        self._theta = self._theta0.clone()
+        self._vel = torch.zeros(6, **kw)
+        self._theta_ready = None  # event on the side stream: the last step's theta update is done
         self.status = torch.zeros(B, dtype=torch.int32, device=self.device)
         self.iters = torch.zeros(2, B, dtype=torch.int32, device=self.device)
         self.log = torch.zeros(_abi.LOG_FIELDS, B, **kw) if write_log else None
@@ -181,7 +184,7 @@ class TubeMPC:
         st.x, st.b, st.xbar, st.bbar = (t.data_ptr() for t in (self.x, self.b, self.xbar, self.bbar))
         st.Xnom, st.Unom, st.Xaux, st.Uaux = (t.data_ptr() for t in (self.Xnom, self.Unom, self.Xaux, self.Uaux))
         st.work = self.work.data_ptr()
-        st.theta = self.theta.data_ptr()
+        st.theta = self._theta.data_ptr()
         st.partials = self.partials.data_ptr()
         st.log = self.log.data_ptr() if self.log is not None else None
         st.status = self.status.data_ptr()
@@ -198,17 +201,17 @@ class TubeMPC:
         # as two launches (dtmpc_tube_state.phase 1: nominal, 2: the rest) and its theta all-reduce + update go to
         # a side stream, which the NEXT step's phase 2 waits on -- so the collective overlaps the next nominal
         # solve and never blocks the launch stream.  Default: on when the step has a cross-rank sum (a process
-        # group of > 1 ranks) and the fused kernel runs it in one chunk; overlap=True forces it (tests).
+        # group of > 1 ranks) and the fused kernel runs it in one chunk of ITS precision (dtmpc_tube_split_ok: the f64
+        # chunk is about half the f32 one); overlap=True forces it (tests).
         import torch.distributed as dist
 
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
-        can = bool(self.lib.dtmpc_tube_split_supported(self._dt, C.byref(self.spec), C.byref(self.cfg), self.lanes)) and \
-            self.B <= self.chunk
+        can = bool(self.lib.dtmpc_tube_split_ok(self._dt, C.byref(self.spec), C.byref(self.cfg), self.B, self.lanes,
+                                                self.chunk))
         if overlap and not can:
-            raise ValueError("overlap needs the fused tube kernel and B <= its launch chunk")
+            raise ValueError("overlap needs the fused tube kernel and B within one launch chunk (dtmpc_tube_split_ok)")
         self.overlap = bool(can and (multi if overlap is None else overlap))
         self._side = torch.cuda.Stream(device=self.device) if self.overlap else None
-        self._theta_ready = None  # event on the side stream: the last step's theta update is done
 
     # -----------------------------------------------------------------------------------------
     def join(self) -> None:
@@ -216,6 +219,26 @@ class TubeMPC:
         vel and sums are the last step's on the current stream.  A no-op otherwise."""
         if self._theta_ready is not None:
             torch.cuda.current_stream(self.device).wait_event(self._theta_ready)
+
+    # the adaptation state: every read (and in-place write) through these orders the current stream after the last
+    # step's theta update, wherever overlap mode put it
+    @property
+    def theta(self) -> Tensor:
+        """[6] shared ancillary weights Qa(3), Ra(2), qba after the last step's update."""
+        self.join()
+        return self._theta
+
+    @property
+    def vel(self) -> Tensor:
+        """[6] momentum of the theta update."""
+        self.join()
+        return self._vel
+
+    @property
+    def sums(self) -> Tensor:
+        """[8] the last step's global sums L, gQ(3), gR(2), gqb, healthy count."""
+        self.join()
+        return self._sums
 
     def reset(self, x0: Tensor, U_nom0: Optional[Tensor] = None, U_aux0: Optional[Tensor] = None) -> None:
         """x0 [B, 3]: plant and nominal start at x0, b0 = B(h(x0)) (core/tube_mpc.py:770-779);
@@ -228,7 +251,7 @@ class TubeMPC:
             x0c = x0.to(device=self.device, dtype=self.dtype).contiguous()
             _lib.check(self.lib.dtmpc_tube_reset(self._dt, C.byref(self.spec), self.B, x0c.data_ptr(),
                                                  C.byref(self.state), self._theta0.data_ptr(),
-                                                 self.theta.data_ptr(), self.vel.data_ptr(), self._stream()),
+                                                 self._theta.data_ptr(), self._vel.data_ptr(), self._stream()),
                        "dtmpc_tube_reset")
             self.t = 0
             return
@@ -244,8 +267,8 @@ class TubeMPC:
             self.Unom.copy_(U_nom0.to(self.Unom).permute(1, 2, 0))
         if U_aux0 is not None:
             self.Uaux.copy_(U_aux0.to(self.Uaux).permute(1, 2, 0))
-        self.theta.copy_(self._theta0)
-        self.vel.zero_()
+        self._theta.copy_(self._theta0)
+        self._vel.zero_()
         self.status.zero_()
         self.t = 0
 
@@ -254,7 +277,10 @@ class TubeMPC:
 
     def step(self, w: Optional[Tensor] = None, kernel_events=None, adapt: bool = True) -> None:
         """One closed-loop step for the whole batch (asynchronous on the current stream).
-        kernel_events: optional (start, end) torch.cuda.Event pair recorded around the fused kernel.
+        kernel_events: optional torch.cuda.Event pair (start, end) recorded around the fused kernel -- in overlap mode
+        a 4-tuple (start1, end1, start2, end2) around its two launches, so that the kernel time (the sum of the two
+        spans) excludes the launch stream's wait for the previous step's theta update, which is end1 -> start2
+        (ADVICE r05); a pair is accepted there too and then spans both launches and the wait.
         adapt=False: theta is held (no partial-sum reduction, all-reduce or update) -- the tube MPC of
         BASELINE config 3 without the adaptation step of config 4; the IFT pass still runs in the fused
         kernel (its per-trajectory rows land in the log)."""
@@ -267,41 +293,48 @@ class TubeMPC:
         s = self._stream()
         if self.costs is not None:  # the kernel writes the candidates that ran: NaN marks the rest
             self.costs.fill_(float("nan"))
-        if kernel_events is not None:
-            kernel_events[0].record()
+        ev = tuple(kernel_events) if kernel_events is not None else ()
+        if len(ev) not in (0, 2, 4):
+            raise ValueError("kernel_events: a (start, end) pair or, in overlap mode, (start1, end1, start2, end2)")
+        if ev:
+            ev[0].record()
         if self.overlap:
             self._launch(1, wp, s)  # the nominal solve: no theta (the side stream may still be updating it)
+            if len(ev) == 4:
+                ev[1].record()
             self.join()
+            if len(ev) == 4:
+                ev[2].record()
             self._launch(2, wp, s)
         else:
             self._launch(0, wp, s)
-        if kernel_events is not None:
-            kernel_events[1].record()
+        if ev:
+            ev[-1].record()
         if not adapt:
             self.t += 1
             return
         if self.overlap:
             _lib.check(self.lib.dtmpc_partials_reduce(self._dt, self.n_partials, self.partials.data_ptr(),
-                                                      self.sums.data_ptr(), s), "dtmpc_partials_reduce")
+                                                      self._sums.data_ptr(), s), "dtmpc_partials_reduce")
             ready = torch.cuda.Event()
             ready.record()
             side = self._side
             side.wait_event(ready)
             with torch.cuda.stream(side):
-                allreduce_sums(self.sums, self.group)  # RCCL's stream waits on `side`, `side` on the collective
-                _lib.check(self.lib.dtmpc_theta_update(self._dt, C.byref(self.adapt), 0.0, self.sums.data_ptr(),
-                                                       self.theta.data_ptr(), self.vel.data_ptr(),
+                allreduce_sums(self._sums, self.group)  # RCCL's stream waits on `side`, `side` on the collective
+                _lib.check(self.lib.dtmpc_theta_update(self._dt, C.byref(self.adapt), 0.0, self._sums.data_ptr(),
+                                                       self._theta.data_ptr(), self._vel.data_ptr(),
                                                        int(side.cuda_stream)), "dtmpc_theta_update")
                 self._theta_ready = torch.cuda.Event()
                 self._theta_ready.record(side)
             self.t += 1
             return
         _lib.check(self.lib.dtmpc_partials_reduce(self._dt, self.n_partials, self.partials.data_ptr(),
-                                                  self.sums.data_ptr(), s), "dtmpc_partials_reduce")
-        allreduce_sums(self.sums, self.group)
+                                                  self._sums.data_ptr(), s), "dtmpc_partials_reduce")
+        allreduce_sums(self._sums, self.group)
         # inv_batch 0: batch mean over the healthy trajectories (sums[7] counts them across ranks)
         _lib.check(self.lib.dtmpc_theta_update(self._dt, C.byref(self.adapt), 0.0,
-                                               self.sums.data_ptr(), self.theta.data_ptr(), self.vel.data_ptr(), s),
+                                               self._sums.data_ptr(), self._theta.data_ptr(), self._vel.data_ptr(), s),
                    "dtmpc_theta_update")
         self.t += 1
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define DTMPC_ABI_VERSION 6
+#define DTMPC_ABI_VERSION 7
 #define DTMPC_MAX_OBS 16
 #define DTMPC_MAX_ALPHAS 8
 #define DTMPC_MAX_HORIZON 512
@@ -171,7 +171,8 @@ typedef struct dtmpc_tube_state {
                        status masking) */
   int32_t* status;  /* [B] DTMPC_ST_* bits (OR-accumulated) */
   int32_t* iters;   /* [2][B] nominal / ancillary iterations used, or NULL */
-  int32_t lanes;    /* lanes per trajectory, fixed when the state is built: dtmpc_tube_lanes(B) */
+  int32_t lanes;    /* lanes per trajectory, fixed when the state is built: dtmpc_tube_lanes_dtype(B, dtype) (the
+                       precision's rule; dtmpc_tube_lanes(B) is the f32 rule) */
   int32_t phase;    /* ABI 6 (was padding, 0): which part of the step dtmpc_tube_step launches -- 0 the whole step;
                        1 the nominal solve alone (theta-independent, core/tube_mpc.py:813-857); 2 the rest (the
                        ancillary solve with the current theta, sensitivity, gradient sums, plant), after a phase-1
@@ -329,6 +330,12 @@ int dtmpc_tube_step(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg
 /* 1 when dtmpc_tube_step runs the fused kernel for this problem / config / precision and lane count, which is
  * what a phase split (dtmpc_tube_state.phase = 1, 2) needs; 0 otherwise.  Host-only. */
 int32_t dtmpc_tube_split_supported(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int32_t lanes);
+/* ABI 7: 1 when a phase split of THIS batch is possible -- dtmpc_tube_split_supported, and B within one launch chunk of
+ * the precision (the nominal records of the whole batch stay in the workspace between the two launches; f64 records
+ * are twice as large, so its chunk is min(chunk, about half the f32 maximum)).  dtmpc_tube_step refuses a phase != 0
+ * launch for which this is 0.  Host-only. */
+int32_t dtmpc_tube_split_ok(int dtype, const dtmpc_spec* spec, const dtmpc_tube_cfg* cfg, int64_t B, int32_t lanes,
+                            int64_t chunk);
 
 /* Episode start of the fused closed loop in one launch (core/tube_mpc.py:770-779; the reference's
  * run_closed_loop_experiment sets x = x_bar = x0, b = b_bar = B(h(x0)), zero warm starts and its

@@ -199,6 +199,44 @@ def test_arguments_validated_before_any_device_call(lib):
     assert rc == _abi.ERR_BAD_ARG
 
 
+def test_split_step_gate_uses_the_precisions_chunk(lib):
+    """a split step (dtmpc_tube_state.phase 1 / 2, TubeMPC overlap) keeps the nominal records of the whole
+    batch in the workspace between its two launches, so B must fit ONE launch chunk of the precision -- and the f64
+    records are twice as large, so its chunk is about half the f32 one.  dtmpc_tube_split_ok (ABI 7) decides it with
+    the clamped chunk; dtmpc_tube_step refuses a phase != 0 launch it rejects, before any device call."""
+    from diff_tube_mpc_strict_pt import _abi
+    from diff_tube_mpc_strict_pt.core.problem import paper_config, paper_setup_from_config
+
+    st = paper_setup_from_config(paper_config())
+    spec = st.problem.to_c()
+    tc = _abi.DtmpcTubeCfg()
+    tc.nominal, tc.nom_ilqr, tc.aux_ilqr = st.nominal_cost.to_c(), st.ilqr_nom.to_c(), st.ilqr_aux.to_c()
+    tc.disturbance = 1  # Philox: no injected w needed
+    c1 = lib.dtmpc_tube_chunk(50, 1)  # the f32 chunk, the one TubeMPC keeps in its state in both precisions
+    per1d = 2 * (51 * 32 + 50 * 96) + 12  # f64 records per trajectory at one lane (see the test above)
+    c1d = (0x7FFFFFFF // per1d) // 256 * 256
+    assert c1d < c1
+    ok = lambda dt, B: lib.dtmpc_tube_split_ok(dt, C.byref(spec), C.byref(tc), B, 1, c1)  # noqa: E731
+    for dt in (_abi.F32, _abi.F64):
+        assert ok(dt, 1000) == 1 and ok(dt, 65536) == 1
+    assert ok(_abi.F32, c1) == 1 and ok(_abi.F32, c1 + 1) == 0
+    assert ok(_abi.F64, c1d) == 1 and ok(_abi.F64, c1d + 1) == 0 and ok(_abi.F64, c1) == 0
+    # the launch refuses it (validation order: state arrays, lanes, partials, workspace, disturbance, then the phase)
+    B = c1d + 256
+    state = _abi.DtmpcTubeState()
+    for f in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux", "Uaux", "work", "theta", "partials", "status"):
+        setattr(state, f, 1)
+    state.lanes, state.chunk, state.phase = 1, c1, 1
+    state.n_partials = lib.dtmpc_tube_partials_count(B, 1)
+    state.work_bytes = lib.dtmpc_tube_workspace_bytes(_abi.F64, 50, B, 1, c1)
+    rc = lib.dtmpc_tube_step(_abi.F64, C.byref(spec), C.byref(tc), B, 0, 0, C.byref(state), None, None)
+    assert rc == _abi.ERR_BAD_ARG and b"split_ok" in lib.dtmpc_last_error()
+    # a non-fused configuration never splits
+    other = st.problem.to_c()
+    other.n_obstacles = 9
+    assert lib.dtmpc_tube_split_ok(_abi.F32, C.byref(other), C.byref(tc), 1000, 1, c1) == 0
+
+
 def test_no_cpu_fallback():
     """The product path refuses host tensors and a missing native library, loudly."""
     import torch

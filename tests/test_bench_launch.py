@@ -38,6 +38,20 @@ def test_bench_self_launches_strong_scaling(n):
     assert d["config"]["parallelism"] == f"dp{n}"
     # value = every rank's trajectories x 31 iterations / the slowest rank's step time
     assert abs(d["value"] - 65536 * 31 / (d["ms_per_step"] * 1e-3)) < 1e-6 * d["value"]
+    # every rank reports itself: shard, kernel time, theta wait, wall time, overlap path, lanes
+    ranks = d["ranks"]
+    assert [r["rank"] for r in ranks] == list(range(n))
+    assert sum(r["batch"] for r in ranks) == 65536 and all(r["batch"] == 65536 // n for r in ranks)
+    for r in ranks:
+        assert r["kernel_ms"] > 0 and r["theta_wait_ms"] >= 0 and r["wall_ms_per_step"] > 0
+        assert r["overlap"] is False  # the dry run's placeholder step has no split launch
+    assert d["kernel_ms_max_over_ranks"] == max(r["kernel_ms"] for r in ranks)
+    assert d["comm"]["backend"] == "gloo" and "all_reduce" in d["comm"]["collective"]
+    assert d["comm"]["theta_wait_ms_max_over_ranks"] == max(r["theta_wait_ms"] for r in ranks)
+    # beside the strong-scaling line, the same step at 65,536 trajectories per GPU (weak scaling)
+    w = d["weak_scaling"]
+    assert w["batch_per_gpu"] == 65536 and w["global_batch"] == 65536 * n
+    assert abs(w["value"] - 65536 * n * 31 / (w["ms_per_step"] * 1e-3)) < 1e-6 * w["value"]
 
 
 def test_bench_weak_scaling_flag():

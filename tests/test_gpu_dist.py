@@ -158,12 +158,16 @@ def test_split_step_overlap_bitwise(monkeypatch, tag, lanes):
                       record_choices=True)
         assert mpc.overlap == ov
         mpc.reset(_x0(0, 1000))
+        # theta / vel / sums read right after step() on the current stream, with no join() and no
+        # device-wide synchronize -- the properties order the read after the side stream's update
+        seen = []
         for _ in range(3):
             mpc.step()
-        mpc.join()
+            seen.append(torch.cat([mpc.theta.clone(), mpc.vel.clone(), mpc.sums.clone()]))
         torch.cuda.synchronize(dev)
         out.append({k: getattr(mpc, k).cpu().numpy().copy() for k in ("x", "b", "xbar", "bbar", "Xnom", "Unom", "Xaux",
                                                                        "Uaux", "theta", "vel", "sums", "status",
                                                                        "iters", "choices")})
+        out[-1]["seen"] = torch.stack(seen).cpu().numpy()
     for k in out[0]:
         assert np.array_equal(out[0][k], out[1][k], equal_nan=True), k
