@@ -113,17 +113,31 @@ def build(force: bool = False, variant: str = "", defines=(), only=(), on_produc
                                ", ".join(f"{k} ({b} B)" for k, b in bad))
         # and no 128-bit record store of a fused kernel may have its data registers written inside its two wait
         # states (the store-data hazard, csrc/dtmpc_fast.hip st128; profiles/r05/store_hazard.txt)
-        haz = {}
+        haz, vh, fc = {}, {}, {}
         for o in objs:
             tu = os.path.basename(o).split(".")[0]
             if tu.startswith("dtmpc_fast"):
                 haz[tu] = [list(h) for h in store_hazards(o)]
+                vh[tu] = [list(h) for h in valu_hazards(o)]
+            fc[tu] = [list(h) for h in flow_copies(o)]  # every unit: the generic kernels branch per lane as well
+        with open(os.path.join(CACHE, "flow_copies.json"), "w") as f:
+            json.dump(fc, f, indent=1, sort_keys=True)
+        nf = sum(len(v) for v in fc.values())
+        if nf and os.environ.get("DTMPC_RESOURCE_STRICT", "1") != "0":
+            raise RuntimeError(f"{nf} vector-register writes in divergent flow blocks (build/obj/flow_copies.json): "
+                               + ", ".join(sorted({h[0] for v in fc.values() for h in v}))[:2000])
         with open(os.path.join(CACHE, "store_hazards.json"), "w") as f:
             json.dump(haz, f, indent=1, sort_keys=True)
+        with open(os.path.join(CACHE, "valu_hazards.json"), "w") as f:
+            json.dump(vh, f, indent=1, sort_keys=True)
         nh = sum(len(v) for v in haz.values())
         if nh and os.environ.get("DTMPC_RESOURCE_STRICT", "1") != "0":
             raise RuntimeError(f"{nh} 128-bit stores with their data registers overwritten inside the hazard window "
                                "(build/obj/store_hazards.json)")
+        nv = sum(len(v) for v in vh.values())
+        if nv and os.environ.get("DTMPC_RESOURCE_STRICT", "1") != "0":
+            raise RuntimeError(f"{nv} wait-state hazards (DPP / readlane / SGPR->VMEM / trans) in the fused kernels "
+                               "(build/obj/valu_hazards.json)")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     print("[build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -233,6 +247,192 @@ def scan_store_hazards(dis: str) -> list:
             if waits >= 2:
                 break
     return out
+
+
+# gfx9 / CDNA4 wait-state rules the compiler pads for its own instructions but not around inline assembly (an asm
+# statement is one opaque instruction to hipcc: cdna_hip_programming.md section 5.7 item 2) -- checked on the final
+# code of every fused kernel, whatever produced it (widen the scan beyond the store-data hazard).
+# (class, wait states the consumer needs after the producer)
+VALU_HAZARDS = {
+    "VALU->DPP": 2,            # a VALU write of a VGPR, then a DPP instruction reading it
+    "VALU->READLANE": 1,       # a VALU write of a VGPR, then v_readlane / v_readfirstlane reading it
+    "VALU_SGPR->VMEM": 5,      # a VALU write of an SGPR (v_readlane, v_readfirstlane, v_cmp, carry-out), then a
+                               # buffer / global instruction reading it (descriptor, soffset, saddr)
+    "VALU_SGPR->LANESEL": 4,   # the same SGPR as the lane select of v_readlane / v_writelane
+    "TRANS->VALU": 1,          # a transcendental (v_exp / log / rcp / rsq / sqrt / sin / cos), then a non-trans VALU reading its result
+}
+_TRANS = r"^v_(exp|log|rcp|rsq|sqrt|sin|cos)_(f16|f32|f64|legacy|iflag)"
+
+
+def _sregs(tok: str):
+    """The SGPR numbers of an operand token (s7, s[6:9]); vcc is s[106:107]."""
+    import re
+
+    tok = tok.strip().rstrip(",")
+    if tok in ("vcc", "vcc_lo"):
+        return {106, 107} if tok == "vcc" else {106}
+    m = re.fullmatch(r"s(\d+)", tok) or re.fullmatch(r"s\[(\d+):(\d+)\]", tok)
+    if not m:
+        return set()
+    lo = int(m.group(1))
+    hi = int(m.group(2)) if m.lastindex == 2 else lo
+    return set(range(lo, hi + 1))
+
+
+def _operands(ins: str):
+    """(opcode, operand tokens) of one disassembled instruction (modifiers such as quad_perm: / offen dropped)."""
+    import re
+
+    ins = ins.split("//")[0].strip()
+    parts = ins.split(None, 1)
+    if len(parts) < 2:
+        return parts[0] if parts else "", []
+    body = re.split(r"\s(?:quad_perm|row_\w+|wave_\w+|offen|idxen|offset|bank_mask|bound_ctrl|sc0|sc1|nt|lds|glc|slc)",
+                    " " + parts[1])[0]
+    return parts[0], [t for t in re.split(r",\s*", body.strip()) if t]
+
+
+def scan_valu_hazards(dis: str, window: int = 6) -> list:
+    """VALU_HAZARDS on a disassembly text (llvm-objdump -d): [(class, kernel, producer, consumer, wait states seen)].
+    Straight-line windows in program order (a branch counts as one wait state and the scan continues on the
+    fall-through path, which over-approximates: a hit is a site to read, and the product has none)."""
+    import re
+
+    out, kern, prog = [], None, []
+    for line in dis.splitlines():
+        m = re.match(r"^<(\S+)>:", line.strip()) if line and not line.startswith((" ", "\t")) else None
+        m = m or re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+        if m:
+            kern = m.group(1)
+            continue
+        if line.startswith("\t") and kern:
+            prog.append((kern, line.strip()))
+    n = len(prog)
+    for i, (k, ins) in enumerate(prog):
+        op, ops = _operands(ins)
+        if not op.startswith("v_") or not ops:
+            continue
+        dv, ds = set(), set()
+        if op.startswith(("v_readlane", "v_readfirstlane", "v_cmp")):
+            ds = _sregs(ops[0])
+        else:
+            dv = _vregs(ops[0])
+            if len(ops) > 1 and re.match(r"v_(add|sub|addc|subb|subrev)_co|v_div_scale|v_mad_[iu]64", op):
+                ds = _sregs(ops[1])
+        trans = re.match(_TRANS, op) is not None
+        w = 0
+        for j in range(i + 1, min(n, i + 1 + window)):
+            k2, ins2 = prog[j]
+            if k2 != k:
+                break
+            op2, ops2 = _operands(ins2)
+            if op2 == "s_endpgm":
+                break
+            rv, rs = set(), set()
+            for t in ops2[1:]:
+                rv |= _vregs(t.rstrip(","))
+                rs |= _sregs(t)
+            if op2.startswith(("buffer_store", "global_store")) and ops2:
+                rv |= _vregs(ops2[0].rstrip(","))
+            hit = None
+            if op2.startswith(("buffer_", "global_")):
+                srs = set()
+                for t in ops2:
+                    srs |= _sregs(t)
+                if ds & srs and w < VALU_HAZARDS["VALU_SGPR->VMEM"]:
+                    hit = "VALU_SGPR->VMEM"
+            elif ("_dpp" in op2 or "quad_perm" in ins2 or "row_" in ins2) and dv & rv and w < VALU_HAZARDS["VALU->DPP"]:
+                hit = "VALU->DPP"
+            elif op2.startswith(("v_readlane", "v_readfirstlane")) and len(ops2) > 1:
+                if dv & _vregs(ops2[1].rstrip(",")) and w < VALU_HAZARDS["VALU->READLANE"]:
+                    hit = "VALU->READLANE"
+                elif len(ops2) > 2 and ds & _sregs(ops2[2]) and w < VALU_HAZARDS["VALU_SGPR->LANESEL"]:
+                    hit = "VALU_SGPR->LANESEL"
+            elif op2.startswith("v_writelane") and len(ops2) > 2 and ds & _sregs(ops2[2]) and \
+                    w < VALU_HAZARDS["VALU_SGPR->LANESEL"]:
+                hit = "VALU_SGPR->LANESEL"
+            elif trans and op2.startswith("v_") and not re.match(_TRANS, op2) and dv & rv and w < VALU_HAZARDS["TRANS->VALU"]:
+                hit = "TRANS->VALU"
+            if hit:
+                out.append((hit, k, ins.split("//")[0].strip(), ins2.split("//")[0].strip(), w))
+            w += int(ops2[0], 0) + 1 if op2 == "s_nop" and ops2 else 1
+            if w >= 5:
+                break
+    return out
+
+
+def valu_hazards(obj: str) -> list:
+    """scan_valu_hazards on the gfx950 code object inside a hipcc object file."""
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        co = _code_object(obj, d)
+        dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", f"--mcpu={ARCH}", "--no-show-raw-insn",
+                              "--no-leading-addr", co], check=True, capture_output=True, text=True).stdout
+    return scan_valu_hazards(dis)
+
+
+def _listing(dis: str):
+    """{kernel: [(instruction, byte offset, branch-target offset or None)]} of an llvm-objdump -d text."""
+    import re
+
+    out, cur = {}, None
+    for line in dis.splitlines():
+        m = re.match(r"^<(\S+)>:", line.strip()) if line and not line.startswith((" ", "\t")) else None
+        m = m or re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+        if m:
+            cur = out.setdefault(m.group(1), [])
+            continue
+        if cur is None or not line.startswith("\t"):
+            continue
+        a = re.search(r"// ([0-9A-F]+):", line)
+        if not a:
+            continue
+        t = re.search(r"<\S+\+0x([0-9a-f]+)>", line)
+        cur.append((line.split("//")[0].strip(), int(a.group(1), 16), int(t.group(1), 16) if t else None))
+    for k, ins in out.items():
+        if ins:
+            b = ins[0][1]
+            out[k] = [(x, a - b, (t - 0) if t is not None else None) for x, a, t in ins]
+    return out
+
+
+def scan_flow_copies(dis: str) -> list:
+    """Vector-register writes in the FLOW block of a divergent if / else (round 6, profiles/r06/flow_copy_root_cause.txt):
+    after `s_and_saveexec_b64 sX, vcc ; s_xor_b64 sX, exec, sX ; s_cbranch_execz FLOW`, the block FLOW is entered on
+    both control paths but runs with the THEN lanes' exec mask until its `s_andn2_saveexec_b64` switches to the else
+    lanes -- so a copy the register allocator places there (a live-range split of a value defined before the branch)
+    reaches the then-lanes only, and the else-lanes later read the register's stale content.  v_writelane /
+    v_readlane (exec-independent SGPR spills) are not writes of this kind.  [(kernel, if offset, instruction)]."""
+    out = []
+    for k, ins in _listing(dis).items():
+        idx = {a: i for i, (_, a, _) in enumerate(ins)}
+        for i in range(len(ins) - 2):
+            if not (ins[i][0].startswith("s_and_saveexec_b64") and ins[i + 1][0].startswith("s_xor_b64")
+                    and "exec" in ins[i + 1][0] and ins[i + 2][0].startswith("s_cbranch_execz")):
+                continue
+            t = ins[i + 2][2]
+            if t not in idx:
+                continue
+            j = idx[t]
+            while j < len(ins) and not ins[j][0].startswith(("s_andn2_saveexec_b64", "s_or_saveexec_b64", "s_or_b64 exec",
+                                                             "s_mov_b64 exec", "s_branch", "s_cbranch", "s_endpgm")):
+                x = ins[j][0]
+                if x.startswith("v_") and not x.startswith(("v_writelane", "v_readlane", "v_readfirstlane", "v_cmp")):
+                    out.append((k, ins[i][1], x))
+                j += 1
+    return out
+
+
+def flow_copies(obj: str) -> list:
+    """scan_flow_copies on the gfx950 code object inside a hipcc object file."""
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        co = _code_object(obj, d)
+        dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", f"--mcpu={ARCH}", "--no-show-raw-insn",
+                              "--no-leading-addr", co], check=True, capture_output=True, text=True).stdout
+    return scan_flow_copies(dis)
 
 
 def check_resources(objs, strict: bool = True) -> dict:

@@ -757,13 +757,27 @@ __device__ __forceinline__ f2 vbarrier(const FP& p, f2 z) {
   return r;
 }
 // _dB_relaxed_inv_dz core/systems/dubins_aug_jac.py:31-40 (dbarrier_relaxed)
+// f64: without a divergent branch -- one IEEE division of a selected numerator and denominator, the same values bit
+// for bit (-(1 / zc^2) = -1 / zc^2 exactly; the relaxed branch's (2 diff) / a3 - 1 / a^2 as written).  The branch
+// form's if / else gave the register allocator a flow block that runs with the then-lanes' exec mask only, and it
+// placed live-range-split copies of long-lived values there: the else-lanes never received them (ROCm 7.2, the
+// round-5 "stale workspace" defect, profiles/r06/flow_copy_root_cause.txt; build.py flow_copies scans for it).
 __device__ __forceinline__ real dbarrier(const FP& p, real z) {
+#if DTMPC_FAST_F64
+  DTMPC_NOCONTRACT
+  const bool inv = z >= p.a;
+  const real zc = z < p.eps ? p.eps : z;
+  const real diff = z - p.a;
+  const real q = (inv ? -1.0 : 2.0 * diff) / (inv ? zc * zc : p.a3);
+  return inv ? q : -p.inv_a2 + q;
+#else
   if (z >= p.a) {
     const real zc = z < p.eps ? p.eps : z;
     return -m_rcp(zc * zc);
   }
   const real diff = z - p.a;
   return -p.inv_a2 + (2.f * diff) / p.a3;
+#endif
 }
 
 // smooth-min h (dubins_obstacles.py:41-69), two passes, the h_i of the first kept (h_smoothmin_w)
@@ -1127,9 +1141,41 @@ __device__ __forceinline__ real init_tape(const FP& p, const FCost& c, const rea
   return J + term<TRACK, Obs<M>::wrap>(c, s0, s1, s2, sb, R.x, R.y, R.z);
 }
 
+// DTMPC_FAST_RIC_FMA = 1 (round 6): the backward step -- this Jacobian and the Riccati step (riccati_pk) -- compiled
+// without implicit contraction, its multiply-adds as explicit fmas at fixed places (rfm / fma2): every rounding of the
+// recursion is written in the source, so the lane forms, the record forms and every code placement get the same bits
+// (with implicit contraction the compiler re-rounded it per call site: DESIGN.md section 3 "Four lanes").
+#ifndef DTMPC_FAST_RIC_FMA
+#define DTMPC_FAST_RIC_FMA 0
+#endif
+// a * b + c as one rounding (RIC_FMA) or two
+__device__ __forceinline__ real rfm(real a, real b, real c) {
+#if DTMPC_FAST_RIC_FMA
+  return __builtin_fma(a, b, c);
+#else
+  DTMPC_NOCONTRACT
+  return a * b + c;
+#endif
+}
+__device__ __forceinline__ f2 rfm2(f2 a, f2 b, f2 c) {
+#if DTMPC_FAST_RIC_FMA
+  return __builtin_elementwise_fma(a, b, c);
+#else
+  DTMPC_NOCONTRACT
+  return a * b + c;
+#endif
+}
+// (a0 b0 + a1 b1 + c) + a3 b3 in the reference's left-to-right order: the P A / S A row sums (and Q_x's) of the step
+__device__ __forceinline__ real rdot3c(real a0, real b0, real a1, real b1, real c, real a3, real b3) {
+  DTMPC_NOCONTRACT
+  return rfm(a3, b3, rfm(a1, b1, a0 * b0) + c);
+}
 // sparse augmented Jacobian (make_jac, core/systems/dubins_aug_jac.py:61-139)
 __device__ __forceinline__ Jac<real> jac(const FP& p, real sn, real cs, real v, real gxk, real gyk, real dBk,
                                           real gxn, real gyn, real dBn) {
+#if DTMPC_FAST_RIC_FMA
+  DTMPC_NOCONTRACT
+#endif
   Jac<real> J;
   const real dt = p.dt;
   J.a02 = -dt * v * sn;
@@ -1139,11 +1185,19 @@ __device__ __forceinline__ Jac<real> jac(const FP& p, real sn, real cs, real v, 
   J.b21 = dt;
   const real r0 = dBn * gxn, r1 = dBn * gyn, r2 = dBn * 0.f;
   const real gd = p.gamma * dBk;
+#if DTMPC_FAST_RIC_FMA
+  J.a30 = rfm(-gd, gxk, r0);
+  J.a31 = rfm(-gd, gyk, r1);
+  J.a32 = (rfm(r1, J.a12, r0 * J.a02) + r2) - gd * 0.f;
+  J.g = p.gamma;
+  J.b30 = rfm(r1, J.b10, r0 * J.b00);
+#else
   J.a30 = r0 - gd * gxk;
   J.a31 = r1 - gd * gyk;
   J.a32 = (r0 * J.a02 + r1 * J.a12 + r2) - gd * 0.f;
   J.g = p.gamma;
   J.b30 = r0 * J.b00 + r1 * J.b10;
+#endif
   J.b31 = r2 * dt;
   return J;
 }
@@ -1174,6 +1228,9 @@ __device__ __forceinline__ f2 bc(real v) { return f2{v, v}; }
 template <bool G0>
 __device__ __forceinline__ bool riccati_pk(const Jac<real>& J, const real* lx, const real* lu, const real* lxx,
                                            const real* luu, real reg, RicP& R, real* K, real* kff) {
+#if DTMPC_FAST_RIC_FMA
+  DTMPC_NOCONTRACT  // every rounding of the step is written below (rfm / fma2): the same bits at every call site
+#endif
   const real a02 = J.a02, a12 = J.a12, a30 = J.a30, a31 = J.a31, a32 = J.a32, g = J.g;
   const real b00 = J.b00, b10 = J.b10, b21 = J.b21, b30 = J.b30, b31 = J.b31;
   const f2 A3 = f2{a30, a31};
@@ -1183,10 +1240,17 @@ __device__ __forceinline__ bool riccati_pk(const Jac<real>& J, const real* lx, c
   const f2 V31 = G0 ? f2{0.f, lxx[3]} : R.V[3][1];
   // Q_x = l_x + A^T V_x ; Q_u = l_u + B^T V_x
   const f2 Qx01 = f2{lx[0], lx[1]} + fma2(A3, bc(vx3), R.Vx[0]);
+#if DTMPC_FAST_RIC_FMA
+  const real Qx2 = lx[2] + rdot3c(a02, vx0, a12, vx1, vx2, a32, vx3);
+  const real Qx3 = G0 ? lx[3] : rfm(g, vx3, lx[3]);
+  const real Qu0 = lu[0] + rfm(b30, vx3, rfm(b10, vx1, b00 * vx0));
+  const real Qu1 = G0 ? rfm(b21, vx2, lu[1]) : lu[1] + rfm(b31, vx3, b21 * vx2);
+#else
   const real Qx2 = lx[2] + (a02 * vx0 + a12 * vx1 + vx2 + a32 * vx3);
   const real Qx3 = G0 ? lx[3] : lx[3] + g * vx3;
   const real Qu0 = lu[0] + (b00 * vx0 + b10 * vx1 + b30 * vx3);
   const real Qu1 = G0 ? lu[1] + b21 * vx2 : lu[1] + (b21 * vx2 + b31 * vx3);
+#endif
   // P = A^T V_xx
   f2 P[4][2];
   if (G0) {
@@ -1213,7 +1277,11 @@ __device__ __forceinline__ bool riccati_pk(const Jac<real>& J, const real* lx, c
   for (int i = 0; i < NR; ++i) {
     const real p0 = P[i][0].x, p1 = P[i][0].y, p2 = P[i][1].x, p3 = P[i][1].y;
     Q[i][0] = fma2(A3, bc(p3), P[i][0]);
+#if DTMPC_FAST_RIC_FMA
+    Q[i][1] = f2{rdot3c(a02, p0, a12, p1, p2, a32, p3), G0 ? 0.f : g * p3};
+#else
     Q[i][1] = f2{a02 * p0 + a12 * p1 + p2 + a32 * p3, G0 ? 0.f : g * p3};
+#endif
   }
   Q[0][0].x = lxx[0] + Q[0][0].x;
   Q[1][0].y = lxx[1] + Q[1][0].y;
@@ -1245,28 +1313,59 @@ __device__ __forceinline__ bool riccati_pk(const Jac<real>& J, const real* lx, c
   for (int a = 0; a < 2; ++a) {
     const real s0 = S[a][0].x, s1 = S[a][0].y, s2 = S[a][1].x, s3 = S[a][1].y;
     Qux[a][0] = fma2(A3, bc(s3), S[a][0]);
+#if DTMPC_FAST_RIC_FMA
+    Qux[a][1] = f2{rdot3c(a02, s0, a12, s1, s2, a32, s3), G0 ? 0.f : g * s3};
+    Quu[a][0] = rfm(s3, b30, rfm(s1, b10, s0 * b00));
+    Quu[a][1] = G0 ? s2 * b21 : rfm(s3, b31, s2 * b21);
+#else
     Qux[a][1] = f2{a02 * s0 + a12 * s1 + s2 + a32 * s3, G0 ? 0.f : g * s3};
     Quu[a][0] = s0 * b00 + s1 * b10 + s3 * b30;
     Quu[a][1] = G0 ? s2 * b21 : s2 * b21 + s3 * b31;
+#endif
   }
   Quu[0][0] = luu[0] + Quu[0][0];
   Quu[1][1] = luu[1] + Quu[1][1];
   // gains with the regularised Q_uu (:239-249): LU with partial pivoting, K = -x, k = -x
+#if DTMPC_FAST_RIC_FMA
+  // lu2 (dtmpc_device.hpp) with its one multiply-add fused: u11 = a11 - l a01
+  LU2<real> f;
+  {
+    const real m00 = Quu[0][0] + reg, m01 = Quu[0][1], m10 = Quu[1][0], m11 = Quu[1][1] + reg;
+    f.sw = m_abs(m10) > m_abs(m00);
+    const real a00 = f.sw ? m10 : m00, a01 = f.sw ? m11 : m01, a10 = f.sw ? m00 : m10, a11 = f.sw ? m01 : m11;
+    f.inv00 = m_rcp(a00);
+    f.l = a10 * f.inv00;
+    f.inv11 = m_rcp(rfm(-f.l, a01, a11));
+    f.a00 = a00;
+    f.a01 = a01;
+  }
+#else
   const LU2<real> f = lu2(Quu[0][0] + reg, Quu[0][1], Quu[1][0], Quu[1][1] + reg);
+#endif
   f2 Kp[2][2];  // K row a, columns (0, 1) and (2, 3)
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const f2 r0 = Qux[0][c], r1 = Qux[1][c];
     const f2 p0 = f2{f.sw ? r1.x : r0.x, f.sw ? r1.y : r0.y}, p1 = f2{f.sw ? r0.x : r1.x, f.sw ? r0.y : r1.y};
+#if DTMPC_FAST_RIC_FMA
+    Kp[1][c] = rfm2(bc(-f.l), p0, p1) * bc(-f.inv11);
+    Kp[0][c] = rfm2(bc(f.a01), Kp[1][c], p0) * bc(-f.inv00);
+#else
     const f2 y1 = p1 - bc(f.l) * p0;
     Kp[1][c] = y1 * bc(-f.inv11);
     Kp[0][c] = (p0 + bc(f.a01) * Kp[1][c]) * bc(-f.inv00);
+#endif
   }
   {
     const real p0 = f.sw ? Qu1 : Qu0, p1 = f.sw ? Qu0 : Qu1;
+#if DTMPC_FAST_RIC_FMA
+    kff[1] = rfm(-f.l, p0, p1) * -f.inv11;
+    kff[0] = rfm(f.a01, kff[1], p0) * -f.inv00;
+#else
     const real y1 = p1 - f.l * p0;
     kff[1] = y1 * -f.inv11;
     kff[0] = (p0 + f.a01 * kff[1]) * -f.inv00;
+#endif
   }
   K[0] = Kp[0][0].x;
   K[1] = Kp[0][0].y;
