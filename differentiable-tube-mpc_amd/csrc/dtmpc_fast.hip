@@ -1146,12 +1146,12 @@ __device__ __forceinline__ real init_tape(const FP& p, const FCost& c, const rea
 // recursion is written in the source, so the lane forms, the record forms and every code placement get the same bits
 // (with implicit contraction the compiler re-rounded it per call site: DESIGN.md section 3 "Four lanes").
 #ifndef DTMPC_FAST_RIC_FMA
-#define DTMPC_FAST_RIC_FMA 0
+#define DTMPC_FAST_RIC_FMA 1
 #endif
 // a * b + c as one rounding (RIC_FMA) or two
 __device__ __forceinline__ real rfm(real a, real b, real c) {
 #if DTMPC_FAST_RIC_FMA
-  return __builtin_fma(a, b, c);
+  return __builtin_elementwise_fma(a, b, c);  // the value type's own fma (__builtin_fma is the double one)
 #else
   DTMPC_NOCONTRACT
   return a * b + c;
@@ -1460,13 +1460,15 @@ __device__ __forceinline__ Lin lin_point(const FP& p, const f4& X) {
 // trajectory, and handed to every lane by DPP broadcasts; the Riccati recursion itself is sequential
 // and runs on every lane (each needs the gains).  Same operations on the same values as P = 1: the
 // gains are bitwise those of the one-lane form.
-// DTMPC_FAST_BW_BCAST (A/B, default off; DESIGN.md section 3 "Small batches: the four-lane step's latency"): at
-// P > 1 the step inputs handed on from the group's per-lane rows by DPP instead of loaded one step ahead.  Same values
-// (bitwise under -ffp-contract=off), but the compiler contracts the Riccati step differently: B = 4,096 2.04 -> 2.02 ms
-// in this form; the in-step broadcast form (round-5 experiment) ran 1.91 ms but its contraction moved the f32
-// gradient rows below the raw-rate parity gate (0.944 < 0.95), so neither is the product.
+// DTMPC_FAST_BW_BCAST (DESIGN.md section 3 "Small batches: the four-lane step's latency"): at P > 1 the step inputs
+// come from the group's per-lane rows by DPP instead of being loaded one step ahead -- 2 (default since round 6): in the
+// step itself, lane j of the group owning row k; 1: handed on one step ahead.  The same values; round 5 left both off
+// because the compiler contracted the Riccati step differently in each form.  Since round 6 the step's rounding is
+// written in the source (DTMPC_FAST_RIC_FMA), so every form gives the same bits (tests/test_gpu_lanes.py) and the
+// in-step form is taken for its latency: B = 4,096 tube step 1.94 -> 1.85 ms, config-2 DDP 0.656 -> 0.630 ms,
+// f64 B = 8,192 4.65 -> 4.29 ms (profiles/r06/ab_ric.txt).
 #ifndef DTMPC_FAST_BW_BCAST
-#define DTMPC_FAST_BW_BCAST 0
+#define DTMPC_FAST_BW_BCAST 2
 #endif
 template <bool TRACK, int M, class SV>
 __device__ __forceinline__ bool backward(const FP& p, const FCost& c, real reg, const SV& S, int h) {
@@ -2770,18 +2772,23 @@ __device__ __forceinline__ FP phase_p() {
 template <int M, int GM>
 constexpr int tab_flag();
 // the exp form of an f64 instantiation: the one-block asm polynomial holds its ten coefficients in VGPRs, which the
-// four-lane kernels and the table-in-kernarg (kLds) ones cannot afford without a private segment (build.py check).
-// One lane only: at two lanes the asm form's closed loop depended on what earlier runs left in the (uninitialised)
-// workspace on one trajectory of 700 (scripts/diag_reuse.py with the workspace pre-filled; the compiled-fma form,
-// and the asm form without the store guard, were clean) -- not root-caused, so that form stays where the same check
-// is clean (tests/test_gpu_reuse.py)
+// table-in-kernarg (kLds) kernels and the four-lane kernels cannot afford without a private segment (build.py check:
+// 48 B of scratch in fk64::tube_fast_kernel<5, 4, 2> beside the in-step broadcast of the backward inputs, in <5, 4, 1>
+// without it), so it runs at one and two lanes.  Round 5 kept it at one lane after the two-lane
+// form read stale values on one trajectory of 700; round 6 found the cause (profiles/r06/flow_copy_root_cause.txt): the
+// register allocator's live-range-split copies in the flow block of dbarrier's divergent if / else, which ran with the
+// then-lanes' exec mask only -- the asm form's extra VGPRs only made the allocator split there.  dbarrier is branchless
+// in f64 now, build.py fails a build with any such copy (scan_flow_copies), and the two-lane asm form (and the
+// four-lane one, where it fits) passes tests/test_gpu_reuse.py (profiles/r06/logs).
 #ifndef DTMPC_FAST64_XASM_MAXP
-#define DTMPC_FAST64_XASM_MAXP 1
+#define DTMPC_FAST64_XASM_MAXP 2
 #endif
 template <int M, int GM, int P>
 constexpr int xasm_flag() {
 #if DTMPC_FAST_F64
-  return (DTMPC_FAST64_EXP == 3 && P <= DTMPC_FAST64_XASM_MAXP && tab_flag<M, GM>() == 0) ? kXasm : 0;
+  return (DTMPC_FAST64_EXP == 3 && P <= DTMPC_FAST64_XASM_MAXP && (P <= 2 || GM == 2) && tab_flag<M, GM>() == 0)
+             ? kXasm
+             : 0;
 #else
   return 0;
 #endif

@@ -18,6 +18,50 @@ from _common import f64_truth, f64_truth_line, oracles, paper_setup, rel_rows, t
 from test_gpu_parity import _oracle_state, _tube_cfg  # noqa: E402
 
 mode = sys.argv[1] if len(sys.argv) > 1 else "bench"
+if mode == "ilqr":
+    # round 6: the RAW per-trajectory agreement rule of tests/test_gpu_parity.py
+    # (test_ilqr_batched_vs_oracle: within max(base, 10 x the builds' spread) of one build; X of the fixed-iteration,
+    # tol-exit and 20-iteration tracking solves, and the gains) measured on valid f32 roundings themselves: each of
+    # plain / fma / ulp against the other two, and the fourth build (liboracle_sym: V_xx mirrored from its upper
+    # triangle, equal in exact arithmetic) against the three -- the device's own setting.  The bar the device can
+    # be held to is what these reach.
+    from _common import agreement, ilqr_cfg
+    from oracle.oracle import Oracle
+    from test_gpu_parity import random_batch
+    from diff_tube_mpc_strict_pt.core import tracking_cost
+
+    st = paper_setup()
+    sp = st.problem.to_c()
+    builds = {v: Oracle(np.float32, nthreads=8, variant=v) for v in ("plain", "fma", "ulp", "sym")}
+    B = 1000
+    x0, V0 = random_batch(B, 5, np.float32)
+    res = {}
+    for cost, mi, tl in ((st.nominal_cost, 5, -1.0), (st.nominal_cost, 10, 1e-3)):
+        res[(mi, tl)] = {v: o.ilqr_solve(sp, cost.to_c(), ilqr_cfg(mi, tl).to_c(), x0, V0) for v, o in builds.items()}
+    Xp, Vp = res[(10, 1e-3)]["plain"][0], res[(10, 1e-3)]["plain"][1]
+    cost = tracking_cost((0.7, 1.3, 0.2, 0.5, 2.0, 0.8))
+    xa = x0.copy()
+    xa[:, :2] += 0.02
+    Va0 = np.roll(Vp, -1, axis=1)
+    res["tracking"] = {v: o.ilqr_solve(sp, cost.to_c(), ilqr_cfg(20, 1e-3).to_c(), xa, Va0, Xp, Vp)
+                       for v, o in builds.items()}
+    print(f"# f32 raw-band calibration, batched iLQR (tests/test_gpu_parity.py test_ilqr_batched_vs_oracle), B = {B}")
+    three = ("plain", "fma", "ulp")
+    for case, r in res.items():
+        keep = np.all([r[v][5] == 0 for v in r], axis=0)
+        for what, k, base in (("X", 0, 1e-3), ("gains", 2, 1e-2)):
+            def arr(v):
+                a = r[v][k][keep]
+                if what == "gains":
+                    a = np.concatenate([a.reshape(len(a), -1), r[v][3][keep].reshape(len(a), -1)], 1)
+                return a
+            line = []
+            for d in three:
+                refs = [arr(v) for v in three if v != d]
+                line.append(f"{d} vs other two {agreement(arr(d), refs, base)[0]:.4f}")
+            line.append(f"sym vs the three {agreement(arr('sym'), [arr(v) for v in three], base)[0]:.4f}")
+            print(f"  [{case}] {what} (base {base:g}, kept {int(keep.sum())}): " + "; ".join(line))
+    sys.exit(0)
 st = paper_setup()
 if mode == "bench":
     st = dataclasses.replace(st, ilqr_nom=dataclasses.replace(st.ilqr_nom, tol=-1.0),

@@ -64,6 +64,10 @@ for s in $STEPS; do
         DTMPC_LIBRARY=$(lib $v) run ab64_b65536_${v}_$rep 300 python bench.py --dtype f64 --steps 5 --warmup 3 --no-cpu --no-steady --no-extra
         DTMPC_LIBRARY=$(lib $v) run ab64_b8192_${v}_$rep 300 python bench.py --dtype f64 --batch 8192 --steps 10 --warmup 5 --no-cpu --no-steady --no-extra
       done; done ;;
+    reusetest)  # VARIANTS: tests/test_gpu_reuse.py (every lane form, f32 and f64) per library
+      for v in ${VARIANTS:-product}; do
+        DTMPC_LIBRARY=$(lib $v) run reusetest_$v 300 python -u -m pytest tests/test_gpu_reuse.py -m gpu -q -rf --timeout 120 --timeout-method thread
+      done ;;
     parity)  # VARIANTS: the tube-step / iLQR oracle gates and the bitwise lane / record / chunk checks per library
       for v in ${VARIANTS:-product}; do
         DTMPC_LIBRARY=$(lib $v) run parity_$v 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_lanes.py -m gpu -q -rf -s --timeout 300 --timeout-method thread -k "${PARITY_K:-tube_step or ilqr_batched or lanes or records}"

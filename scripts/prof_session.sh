@@ -1,10 +1,10 @@
 #!/usr/bin/env bash
-# Round-5 profile session (GPU box), every bench leg's dominant kernel: rocprofv3 --kernel-trace --stats of the
+# Profile session (GPU box; rounds 5-6, ROUND=r06 by default), every bench leg's dominant kernel: rocprofv3 --kernel-trace --stats of the
 # leg's own bench invocation (scripts/trace_summary.py: the timed launches' mean), then one --pmc pass per counter
 # group (no trace domains with --pmc): calibrated HBM bytes (FETCH_SIZE / WRITE_SIZE against the known-byte
 # record_stream_kernel) and the issue counters (SQ_INSTS_VALU per wave, GRBM_GUI_ACTIVE) bench.py turns into the
 # HBM roofline's `traffic` and the `issue` roofline (scripts/pmc_summary.py; bench.py matches workload, batch and
-# the library's sha256).  usage: bash scripts/prof_r05.sh TAG [LEG...]   (legs: tube tube_f64 tube_b4096
+# the library's sha256).  usage: [ROUND=r06] bash scripts/prof_session.sh TAG [LEG...]   (legs: tube tube_f64 tube_b4096
 # nominal_ddp_f32 nominal_ddp_f64 receding_f32 receding_f64; default all)
 set -u
 TAG=${1:-v1}
@@ -12,7 +12,7 @@ shift
 LEGS=${*:-tube tube_f64 tube_b4096 nominal_ddp_f32 nominal_ddp_f64 receding_f32 receding_f64}
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof5_$TAG
+OUT=gpurun_out/prof_${ROUND:-r06}_$TAG
 mkdir -p "$OUT"
 run() {
   echo "[prof] $*"
