@@ -261,13 +261,14 @@ int tube_block(int64_t B, int lanes) {
 
 // f64 (round 5): the fused f64 step is instruction-bound at every batch (no packed f64 VALU), so four lanes --
 // the line search split four ways, the linearisation shared -- pay for their duplicated Riccati recursion up to
-// 4 B <= slots (B <= 16,384: 8.11 ms at four lanes vs 8.83 at two, profiles/r04/f64_lanes_v5.txt); above it one
-// lane (B = 65,536: 13.7 ms vs 19.1 at two, 37.5 at four).
+// 4 B <= slots (B <= 16,384: 8.11 ms at four lanes vs 8.83 at two, profiles/r04/f64_lanes_v5.txt); round 6: two lanes
+// while 2 B <= slots (B = 32,768: 7.36 ms at two lanes vs 9.87 at one, profiles/r06/f64_lanes_v1.txt), above it one
+// lane (B = 65,536: 11.45 ms vs 14.95 at two).
 static int tube_lanes_default(int64_t B, int dtype = DTMPC_F32) {
   const char* e = getenv("DTMPC_TUBE_LANES");
   if (e && (e[0] == '1' || e[0] == '2' || e[0] == '4') && e[1] == 0) return e[0] - '0';
   const int64_t slots = lane_slots();
-  if (dtype == DTMPC_F64) return 4 * B <= slots ? 4 : 1;
+  if (dtype == DTMPC_F64) return 4 * B <= slots ? 4 : 2 * B <= slots ? 2 : 1;
   return 8 * B <= slots ? 4 : 2 * B <= slots ? 2 : 1;
 }
 

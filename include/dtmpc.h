@@ -308,8 +308,8 @@ size_t dtmpc_tube_workspace_bytes(int dtype, int32_t horizon, int64_t B, int32_t
  * dtmpc_tube_step never reads the environment. */
 int32_t dtmpc_tube_lanes(int64_t B);
 /* dtmpc_tube_lanes for a precision (ABI 6): DTMPC_F32 as dtmpc_tube_lanes; DTMPC_F64 4 while 4 B <= slots
- * (B <= 16,384 on MI355X), else 1 -- the f64 step is instruction-bound, so the split line search pays for the
- * duplicated recursion up to a quarter of the lane slots.  The default of dtmpc_ilqr_workspace_bytes /
+ * (B <= 16,384 on MI355X), 2 while 2 B <= slots (B <= 32,768; round 6), else 1 -- the f64 step is
+ * instruction-bound, so the split line search pays for the duplicated recursion up to half the lane slots.  The default of dtmpc_ilqr_workspace_bytes /
  * dtmpc_ilqr_solve_ws (lanes = 0) follows their dtype the same way.  0 for a bad dtype. */
 int32_t dtmpc_tube_lanes_dtype(int64_t B, int dtype);
 /* Number of per-workgroup partial records dtmpc_tube_step writes for B trajectories at `lanes`

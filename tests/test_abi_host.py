@@ -148,10 +148,10 @@ def test_arguments_validated_before_any_device_call(lib):
     assert lib.dtmpc_tube_partials_count(1000, 4) == 63
     assert lib.dtmpc_tube_lanes(65536) in (1, 2, 4) and lib.dtmpc_tube_lanes(4096) in (1, 2, 4)
     # ABI 6: the precision's rule (no device: the MI355X lane slots, 65,536) -- f32 as dtmpc_tube_lanes, f64 four
-    # lanes up to a quarter of the slots, then one
+    # lanes up to a quarter of the slots, two up to half (round 6), then one
     if not os.environ.get("DTMPC_TUBE_LANES"):
         assert [lib.dtmpc_tube_lanes_dtype(b, 0) for b in (4096, 16384, 65536)] == [4, 2, 1]
-        assert [lib.dtmpc_tube_lanes_dtype(b, 1) for b in (4096, 16384, 32768, 65536)] == [4, 4, 1, 1]
+        assert [lib.dtmpc_tube_lanes_dtype(b, 1) for b in (4096, 16384, 32768, 65536)] == [4, 4, 2, 1]
         assert lib.dtmpc_tube_lanes_dtype(4096, 7) == 0
     # the lane count and the partials size come from the state (resolved once by the caller)
     tc.aux_ilqr = st.ilqr_aux.to_c()
