@@ -19,7 +19,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f)
-        for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_fast64.hip", "dtmpc_fast64_ilqr.hip", "dtmpc_fast64_general.hip", "dtmpc_fast_ilqr.hip", "dtmpc_fast_general.hip", "dtmpc_general.hip", "dtmpc_receding.hip",
+        for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_fast_p1.hip", "dtmpc_fast64.hip", "dtmpc_fast64_p1.hip",
+                  "dtmpc_fast64_ilqr.hip", "dtmpc_fast64_general.hip", "dtmpc_fast_ilqr.hip", "dtmpc_fast_general.hip", "dtmpc_general.hip", "dtmpc_receding.hip",
                   "dtmpc_control.hip", "dtmpc_ocp.hip", "dtmpc_systems.hip")]
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solver.hpp", "dtmpc_general.hpp",
                                                  "dtmpc_host.hpp", "dtmpc_ls_pk.hpp")] + [
@@ -30,6 +31,11 @@ CACHE = os.path.join(HERE, "build", "obj")  # object cache keyed by the command 
 ARCH = os.environ.get("DTMPC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
+# per-unit flags: the one-lane tube kernels (one wave per SIMD at the headline batch, nothing to hide a stall behind)
+# with LLVM's iterative ILP scheduler -- same-box A/B in profiles/r06/ab_sched.txt; the multi-lane forms lost with it
+# and the f32 standalone-iLQR / receding unit (config 2 -1.3 %, receding -0.8 %; its f64 twin lost 1.2 % and keeps the default)
+UNIT_FLAGS = {u: ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+              for u in ("dtmpc_fast_p1", "dtmpc_fast64_p1", "dtmpc_fast_ilqr")}
 
 
 def _lib_key() -> str:
@@ -37,7 +43,8 @@ def _lib_key() -> str:
     source edited while a build runs must not leave a stale library that looks up to date)."""
     h = hashlib.sha256(open(__file__, "rb").read())
     for src in SRCS:
-        h.update(_key([HIPCC, *FLAGS, "-c"], src).encode())
+        tu = os.path.splitext(os.path.basename(src))[0]
+        h.update(_key([HIPCC, *FLAGS, *UNIT_FLAGS.get(tu, []), "-c"], src).encode())
     return h.hexdigest()
 
 
@@ -89,17 +96,24 @@ def build(force: bool = False, variant: str = "", defines=(), only=(), on_produc
             continue
         extra = os.environ.get("DTMPC_EXTRA_FLAGS", "").split() if variant and reach else []
         defs = [f"-D{d}" for d in defines] if reach else []
-        cmd = [HIPCC, *FLAGS, *extra, *defs, "-c"]
+        # DTMPC_NO_UNIT_FLAGS=1 (variants only): the units without their UNIT_FLAGS, for the A/B that keeps them
+        uf = [] if variant and os.environ.get("DTMPC_NO_UNIT_FLAGS") == "1" and reach else UNIT_FLAGS.get(tu, [])
+        cmd = [HIPCC, *FLAGS, *uf, *extra, *defs, "-c"]
         obj = os.path.join(CACHE, f"{tu}.{_key(cmd, src)}.o")
         objs.append(obj)
         if os.path.exists(obj):  # content-keyed: safe to reuse even under --force
             continue
         full = [*cmd, "-o", obj + ".tmp", src]
         print("[build]", " ".join(full), flush=True)
-        procs.append((subprocess.Popen(full), obj))
-    if any([p.wait() != 0 for p, _ in procs]):
+        procs.append((subprocess.Popen(full), obj, cmd, src))
+    if any([p.wait() != 0 for p, *_ in procs]):
         raise subprocess.CalledProcessError(1, "hipcc")
-    for _, obj in procs:
+    for _, obj, cmd, src in procs:
+        # hipcc reads the source once for the device pass and again for the host pass, minutes apart: an object whose
+        # sources changed meanwhile would pair one text's kernels with another's launchers under the first text's key
+        if os.path.basename(obj).split(".")[1] != _key(cmd, src):
+            os.remove(obj + ".tmp")
+            raise RuntimeError(f"{src} or a header it includes changed during the build; run it again")
         os.replace(obj + ".tmp", obj)
     if not variant:  # the product: no f64 fused kernel may keep anything in scratch (check_resources)
         import json
@@ -154,7 +168,7 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 # f64 fused units: every kernel must run without a private segment (round 5) -- the f64
 # defects of rounds 3-4 (wrong results, run-to-run differences, an illegal address) came only from f64 fused
 # kernels whose per-lane divergent loops spilled VGPRs to scratch or kept results in scratch through a pointer
-RESOURCE_CHECKED = ("dtmpc_fast64", "dtmpc_fast64_ilqr", "dtmpc_fast64_general")
+RESOURCE_CHECKED = ("dtmpc_fast64", "dtmpc_fast64_p1", "dtmpc_fast64_ilqr", "dtmpc_fast64_general")
 
 
 def kernel_resources(obj: str) -> dict:

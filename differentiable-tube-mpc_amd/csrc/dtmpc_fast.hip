@@ -27,8 +27,18 @@
 
 // this file is the tube step's translation unit; dtmpc_fast_ilqr.hip / dtmpc_fast_general.hip include it
 // for the standalone iLQR's and the general path's instantiations (their host parts below)
-#if defined(DTMPC_FAST_ILQR_TU) || defined(DTMPC_FAST_GENERAL_TU)
+#if defined(DTMPC_FAST_ILQR_TU) || defined(DTMPC_FAST_GENERAL_TU) || defined(DTMPC_FAST_P1_TU)
 #define DTMPC_FAST_AUX_TU 1
+#endif
+// The one-lane tube kernels (the headline's form) live in their own translation units (dtmpc_fast_p1.hip,
+// dtmpc_fast64_p1.hip), compiled with LLVM's iterative ILP scheduler (build.py UNIT_FLAGS): at one wave per SIMD
+// no other wave hides a dependency stall, so the schedule that shortens the chains wins there, while the two- and
+// four-lane forms keep the default scheduler (round-6 A/B, profiles/r06/ab_sched.txt).  Profiling and ISA-only
+// builds keep every form in this unit (the phase counters are this unit's symbols).
+#if !defined(DTMPC_PROFILE) && !defined(DTMPC_FAST_ISA_ONLY) && !defined(DTMPC_FAST_P1_INLINE)
+#define DTMPC_FAST_P1_SPLIT 1
+#else
+#define DTMPC_FAST_P1_SPLIT 0
 #endif
 
 // DTMPC_FAST_F64 = 1 (csrc/dtmpc_fast64.hip): the same kernels in f64, the reference's configured precision
@@ -3532,6 +3542,11 @@ static void fast_p(const dtmpc_spec* sp, FK_NS::FP& p) {
   }
 }
 
+#if DTMPC_FAST_P1_SPLIT
+// the one-lane launches of the tube step (dtmpc_fast_p1.hip / dtmpc_fast64_p1.hip): M obstacles, record form g0
+int FKN(launch_tube_fast_p1)(int M, int g0, dim3 grid, unsigned bs, hipStream_t st, const FK_NS::FK& kk);
+#endif
+
 #ifndef DTMPC_FAST_AUX_TU  // the tube step (this file's own translation unit)
 
 // The fast kernel's configuration: f32, smooth-min over 1..8 obstacles, relaxed inverse barrier,
@@ -3703,9 +3718,15 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
     } else if (lanes == 2) {                                                                               \
       FAST_LANES(m, 2)                                                                                     \
     } else {                                                                                               \
-      FAST_LANES(m, 1)                                                                                     \
+      FAST_LANES_P1(m)                                                                                     \
     }                                                                                                      \
     break;
+#endif
+#if DTMPC_FAST_P1_SPLIT
+#define FAST_LANES_P1(m) \
+  if (int r = FKN(launch_tube_fast_p1)(m, g0, grid, bs, st, kk)) return r;
+#else
+#define FAST_LANES_P1(m) FAST_LANES(m, 1)
 #endif
     switch (sp->n_obstacles) {
 #ifdef DTMPC_FAST_M_ONLY
@@ -3716,11 +3737,36 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
       default: return set_err(DTMPC_ERR_BAD_ARG, "fast tube step: obstacle count not instantiated");
     }
 #undef FAST_CASE
+#undef FAST_LANES_P1
 #undef FAST_LANES
 #undef FAST_LAUNCH
   }
   return check_launch("tube_fast_kernel");
 }
+
+#elif defined(DTMPC_FAST_P1_TU)  // the one-lane tube kernels (csrc/dtmpc_fast_p1.hip, dtmpc_fast64_p1.hip)
+
+#if DTMPC_FAST_P1_SPLIT
+int FKN(launch_tube_fast_p1)(int M, int g0, dim3 grid, unsigned bs, hipStream_t st, const FK_NS::FK& kk) {
+#define P1_LAUNCH(m, g) hipLaunchKernelGGL((FK_NS::tube_fast_kernel<m, 1, g>), grid, dim3(bs), 0, st, kk)
+#define P1_CASE(m)                                        \
+  case m:                                                 \
+    if (g0 == 2) P1_LAUNCH(m, 2);                         \
+    else if (g0) P1_LAUNCH(m, 1);                         \
+    else P1_LAUNCH(m, 0);                                 \
+    return 0;
+  switch (M) {
+#ifdef DTMPC_FAST_M_ONLY
+    P1_CASE(DTMPC_FAST_M_ONLY)
+#else
+    P1_CASE(1) P1_CASE(2) P1_CASE(3) P1_CASE(4) P1_CASE(5) P1_CASE(6) P1_CASE(7) P1_CASE(8)
+#endif
+    default: return set_err(DTMPC_ERR_BAD_ARG, "fast tube step: obstacle count not instantiated");
+  }
+#undef P1_CASE
+#undef P1_LAUNCH
+}
+#endif
 
 #elif defined(DTMPC_FAST_ILQR_TU)  // the standalone iLQR (csrc/dtmpc_fast_ilqr.hip)
 
