@@ -19,7 +19,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRCS = [os.path.join(HERE, "csrc", f)
-        for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_fast_p1.hip", "dtmpc_fast64.hip", "dtmpc_fast64_p1.hip",
+        for f in ("dtmpc_kernels.hip", "dtmpc_fast.hip", "dtmpc_fast_ilp.hip", "dtmpc_fast64.hip", "dtmpc_fast64_ilp.hip",
                   "dtmpc_fast64_ilqr.hip", "dtmpc_fast64_general.hip", "dtmpc_fast_ilqr.hip", "dtmpc_fast_general.hip", "dtmpc_general.hip", "dtmpc_receding.hip",
                   "dtmpc_control.hip", "dtmpc_ocp.hip", "dtmpc_systems.hip")]
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("dtmpc_device.hpp", "dtmpc_solver.hpp", "dtmpc_general.hpp",
@@ -31,11 +31,12 @@ CACHE = os.path.join(HERE, "build", "obj")  # object cache keyed by the command 
 ARCH = os.environ.get("DTMPC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function"]
-# per-unit flags: the one-lane tube kernels (one wave per SIMD at the headline batch, nothing to hide a stall behind)
-# with LLVM's iterative ILP scheduler -- same-box A/B in profiles/r06/ab_sched.txt; the multi-lane forms lost with it
+# per-unit flags: the one-lane tube kernels (one wave per SIMD at the headline batch, nothing to hide a stall behind) and
+# the f32 two-lane ones with LLVM's iterative ILP scheduler -- same-box A/B in profiles/r06/ab_sched.txt; the four-lane
+# forms lost with it
 # and the f32 standalone-iLQR / receding unit (config 2 -1.3 %, receding -0.8 %; its f64 twin lost 1.2 % and keeps the default)
 UNIT_FLAGS = {u: ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
-              for u in ("dtmpc_fast_p1", "dtmpc_fast64_p1", "dtmpc_fast_ilqr")}
+              for u in ("dtmpc_fast_ilp", "dtmpc_fast64_ilp", "dtmpc_fast_ilqr")}
 
 
 def _lib_key() -> str:
@@ -168,7 +169,7 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 # f64 fused units: every kernel must run without a private segment (round 5) -- the f64
 # defects of rounds 3-4 (wrong results, run-to-run differences, an illegal address) came only from f64 fused
 # kernels whose per-lane divergent loops spilled VGPRs to scratch or kept results in scratch through a pointer
-RESOURCE_CHECKED = ("dtmpc_fast64", "dtmpc_fast64_p1", "dtmpc_fast64_ilqr", "dtmpc_fast64_general")
+RESOURCE_CHECKED = ("dtmpc_fast64", "dtmpc_fast64_ilp", "dtmpc_fast64_ilqr", "dtmpc_fast64_general")
 
 
 def kernel_resources(obj: str) -> dict:

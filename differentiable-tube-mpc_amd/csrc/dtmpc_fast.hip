@@ -27,19 +27,21 @@
 
 // this file is the tube step's translation unit; dtmpc_fast_ilqr.hip / dtmpc_fast_general.hip include it
 // for the standalone iLQR's and the general path's instantiations (their host parts below)
-#if defined(DTMPC_FAST_ILQR_TU) || defined(DTMPC_FAST_GENERAL_TU) || defined(DTMPC_FAST_P1_TU)
+#if defined(DTMPC_FAST_ILQR_TU) || defined(DTMPC_FAST_GENERAL_TU) || defined(DTMPC_FAST_ILP_TU)
 #define DTMPC_FAST_AUX_TU 1
 #endif
-// The one-lane tube kernels (the headline's form) live in their own translation units (dtmpc_fast_p1.hip,
-// dtmpc_fast64_p1.hip), compiled with LLVM's iterative ILP scheduler (build.py UNIT_FLAGS): at one wave per SIMD
-// no other wave hides a dependency stall, so the schedule that shortens the chains wins there, while the two- and
-// four-lane forms keep the default scheduler (round-6 A/B, profiles/r06/ab_sched.txt).  Profiling and ISA-only
-// builds keep every form in this unit (the phase counters are this unit's symbols).
-#if !defined(DTMPC_PROFILE) && !defined(DTMPC_FAST_ISA_ONLY) && !defined(DTMPC_FAST_P1_INLINE)
-#define DTMPC_FAST_P1_SPLIT 1
+// The one-lane tube kernels (the headline's form) and the f32 two-lane ones live in their own translation units
+// (dtmpc_fast_ilp.hip, dtmpc_fast64_ilp.hip), compiled with LLVM's iterative ILP scheduler (build.py UNIT_FLAGS): at
+// one or two waves per SIMD little hides a wave's own wait states, so the schedule that shortens the chains wins
+// there, while the four-lane forms (and the f64 two-lane one, even) keep the default scheduler (round-6 A/B,
+// profiles/r06/ab_sched.txt).  Profiling and ISA-only builds keep every form in this unit (the phase counters are
+// this unit's symbols).
+#if !defined(DTMPC_PROFILE) && !defined(DTMPC_FAST_ISA_ONLY) && !defined(DTMPC_FAST_ILP_INLINE)
+#define DTMPC_FAST_ILP_SPLIT 1
 #else
-#define DTMPC_FAST_P1_SPLIT 0
+#define DTMPC_FAST_ILP_SPLIT 0
 #endif
+#define DTMPC_FAST_ILP_P2 (DTMPC_FAST_ILP_SPLIT && !DTMPC_FAST_F64)  // the two-lane form in the split unit too
 
 // DTMPC_FAST_F64 = 1 (csrc/dtmpc_fast64.hip): the same kernels in f64, the reference's configured precision
 // (configs/dubins.yaml:8) -- `real` is the value type of every tape, record and register, ES its size in
@@ -3542,9 +3544,10 @@ static void fast_p(const dtmpc_spec* sp, FK_NS::FP& p) {
   }
 }
 
-#if DTMPC_FAST_P1_SPLIT
-// the one-lane launches of the tube step (dtmpc_fast_p1.hip / dtmpc_fast64_p1.hip): M obstacles, record form g0
-int FKN(launch_tube_fast_p1)(int M, int g0, dim3 grid, unsigned bs, hipStream_t st, const FK_NS::FK& kk);
+#if DTMPC_FAST_ILP_SPLIT
+// the tube step's launches of the split units (dtmpc_fast_ilp.hip / dtmpc_fast64_ilp.hip): M obstacles, lanes 1 (or
+// 2 where DTMPC_FAST_ILP_P2), record form g0
+int FKN(launch_tube_fast_ilp)(int M, int lanes, int g0, dim3 grid, unsigned bs, hipStream_t st, const FK_NS::FK& kk);
 #endif
 
 #ifndef DTMPC_FAST_AUX_TU  // the tube step (this file's own translation unit)
@@ -3716,17 +3719,23 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
     if (lanes == 4) {                                                                                      \
       FAST_LANES(m, 4)                                                                                     \
     } else if (lanes == 2) {                                                                               \
-      FAST_LANES(m, 2)                                                                                     \
+      FAST_LANES_P2(m)                                                                                     \
     } else {                                                                                               \
       FAST_LANES_P1(m)                                                                                     \
     }                                                                                                      \
     break;
 #endif
-#if DTMPC_FAST_P1_SPLIT
+#if DTMPC_FAST_ILP_SPLIT
 #define FAST_LANES_P1(m) \
-  if (int r = FKN(launch_tube_fast_p1)(m, g0, grid, bs, st, kk)) return r;
+  if (int r = FKN(launch_tube_fast_ilp)(m, 1, g0, grid, bs, st, kk)) return r;
 #else
 #define FAST_LANES_P1(m) FAST_LANES(m, 1)
+#endif
+#if DTMPC_FAST_ILP_P2
+#define FAST_LANES_P2(m) \
+  if (int r = FKN(launch_tube_fast_ilp)(m, 2, g0, grid, bs, st, kk)) return r;
+#else
+#define FAST_LANES_P2(m) FAST_LANES(m, 2)
 #endif
     switch (sp->n_obstacles) {
 #ifdef DTMPC_FAST_M_ONLY
@@ -3737,6 +3746,7 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
       default: return set_err(DTMPC_ERR_BAD_ARG, "fast tube step: obstacle count not instantiated");
     }
 #undef FAST_CASE
+#undef FAST_LANES_P2
 #undef FAST_LANES_P1
 #undef FAST_LANES
 #undef FAST_LAUNCH
@@ -3744,27 +3754,40 @@ int FKN(launch_tube_fast)(const dtmpc_spec* sp, const dtmpc_tube_cfg* cf, int64_
   return check_launch("tube_fast_kernel");
 }
 
-#elif defined(DTMPC_FAST_P1_TU)  // the one-lane tube kernels (csrc/dtmpc_fast_p1.hip, dtmpc_fast64_p1.hip)
+#elif defined(DTMPC_FAST_ILP_TU)  // the split units' tube kernels (csrc/dtmpc_fast_ilp.hip, dtmpc_fast64_ilp.hip)
 
-#if DTMPC_FAST_P1_SPLIT
-int FKN(launch_tube_fast_p1)(int M, int g0, dim3 grid, unsigned bs, hipStream_t st, const FK_NS::FK& kk) {
-#define P1_LAUNCH(m, g) hipLaunchKernelGGL((FK_NS::tube_fast_kernel<m, 1, g>), grid, dim3(bs), 0, st, kk)
-#define P1_CASE(m)                                        \
-  case m:                                                 \
-    if (g0 == 2) P1_LAUNCH(m, 2);                         \
-    else if (g0) P1_LAUNCH(m, 1);                         \
-    else P1_LAUNCH(m, 0);                                 \
+#if DTMPC_FAST_ILP_SPLIT
+int FKN(launch_tube_fast_ilp)(int M, int lanes, int g0, dim3 grid, unsigned bs, hipStream_t st, const FK_NS::FK& kk) {
+#define ILP_LAUNCH(m, l, g) hipLaunchKernelGGL((FK_NS::tube_fast_kernel<m, l, g>), grid, dim3(bs), 0, st, kk)
+#define ILP_LANES(m, l) \
+  if (g0 == 2) ILP_LAUNCH(m, l, 2); else if (g0) ILP_LAUNCH(m, l, 1); else ILP_LAUNCH(m, l, 0);
+#if DTMPC_FAST_ILP_P2
+#define ILP_CASE(m)         \
+  case m:                   \
+    if (lanes == 2) {       \
+      ILP_LANES(m, 2)       \
+    } else {                \
+      ILP_LANES(m, 1)       \
+    }                       \
     return 0;
+#else
+#define ILP_CASE(m) \
+  case m:           \
+    ILP_LANES(m, 1) \
+    return 0;
+#endif
+  if (lanes != 1 && !(DTMPC_FAST_ILP_P2 && lanes == 2)) return set_err(DTMPC_ERR_BAD_ARG, "split tube unit: lanes");
   switch (M) {
 #ifdef DTMPC_FAST_M_ONLY
-    P1_CASE(DTMPC_FAST_M_ONLY)
+    ILP_CASE(DTMPC_FAST_M_ONLY)
 #else
-    P1_CASE(1) P1_CASE(2) P1_CASE(3) P1_CASE(4) P1_CASE(5) P1_CASE(6) P1_CASE(7) P1_CASE(8)
+    ILP_CASE(1) ILP_CASE(2) ILP_CASE(3) ILP_CASE(4) ILP_CASE(5) ILP_CASE(6) ILP_CASE(7) ILP_CASE(8)
 #endif
     default: return set_err(DTMPC_ERR_BAD_ARG, "fast tube step: obstacle count not instantiated");
   }
-#undef P1_CASE
-#undef P1_LAUNCH
+#undef ILP_CASE
+#undef ILP_LANES
+#undef ILP_LAUNCH
 }
 #endif
 

@@ -15,6 +15,9 @@ for rep in $(seq 1 "${REPS:-3}"); do for leg in ${LEGS:-h}; do for v in ${VARIAN
     h) args="--steps 40 --warmup 8 $Q" ;;
     b4096) args="--batch 4096 --steps 40 --warmup 8 $Q" ;;
     b8192) args="--batch 8192 --steps 40 --warmup 8 $Q" ;;
+    b16384) args="--batch 16384 --steps 40 --warmup 8 $Q" ;;
+    b32768) args="--batch 32768 --steps 40 --warmup 8 $Q" ;;
+    f64b32768) args="--dtype f64 --batch 32768 --steps 10 --warmup 3 $Q" ;;
     f64) args="--dtype f64 --steps 8 --warmup 3 $Q" ;;
     f64b8192) args="--dtype f64 --batch 8192 --steps 20 --warmup 5 $Q" ;;
     ddp) args="--workload nominal-ddp --dtype f32 --steps 20 --warmup 5" ;;
