@@ -34,9 +34,10 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-Wall", "-Wno-
 # per-unit flags: the one-lane tube kernels (one wave per SIMD at the headline batch, nothing to hide a stall behind) and
 # the f32 two-lane ones with LLVM's iterative ILP scheduler -- same-box A/B in profiles/r06/ab_sched.txt; the four-lane
 # forms lost with it
-# and the f32 standalone-iLQR / receding unit (config 2 -1.3 %, receding -0.8 %; its f64 twin lost 1.2 % and keeps the default)
+# and the f32 standalone-iLQR / receding unit (config 2 -1.3 %, receding -0.8 %; its f64 twin lost 1.2 % and keeps the
+# default) and the f32 general-path unit (general IFT step -1.1 %)
 UNIT_FLAGS = {u: ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
-              for u in ("dtmpc_fast_ilp", "dtmpc_fast64_ilp", "dtmpc_fast_ilqr")}
+              for u in ("dtmpc_fast_ilp", "dtmpc_fast64_ilp", "dtmpc_fast_ilqr", "dtmpc_fast_general")}
 
 
 def _lib_key() -> str:
