@@ -136,3 +136,24 @@ def test_product_objects_have_no_flow_block_copy():
         pytest.skip("no product build with the flow-block scan in this tree (build.py writes build/obj/flow_copies.json)")
     rep = json.load(open(path))
     assert rep and all(len(v) == 0 for v in rep.values()), {k: len(v) for k, v in rep.items() if v}
+
+
+def test_unit_flags_and_checked_units_are_built_units():
+    """UNIT_FLAGS (the iterative-ILP units, DESIGN.md section 3 "The one-lane kernels' instruction schedule") and the
+    f64 resource check name translation units the build compiles: a renamed unit must not silently lose its flags or
+    its scratch check."""
+    units = {os.path.splitext(os.path.basename(s))[0] for s in build.SRCS}
+    assert set(build.UNIT_FLAGS) <= units, set(build.UNIT_FLAGS) - units
+    assert set(build.RESOURCE_CHECKED) <= units, set(build.RESOURCE_CHECKED) - units
+    assert {"dtmpc_fast_ilp", "dtmpc_fast64_ilp"} <= set(build.UNIT_FLAGS)
+    assert "dtmpc_fast64_ilp" in build.RESOURCE_CHECKED
+
+
+def test_object_key_follows_the_source(tmp_path):
+    """build._key covers the source text: the check that refuses an object whose sources changed while hipcc ran
+    (device and host passes read the file minutes apart) compares the key before and after the compile."""
+    src = tmp_path / "x.hip"
+    src.write_text("int a;\n")
+    k0 = build._key(["hipcc", "-c"], str(src))
+    src.write_text("int b;\n")
+    assert build._key(["hipcc", "-c"], str(src)) != k0
